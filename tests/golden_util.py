@@ -1,0 +1,93 @@
+"""Helpers to read the committed golden fixtures (tests/golden/*.json, made by make_golden.py)."""
+from __future__ import annotations
+
+import hashlib
+import json
+import math
+import os
+import struct
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as fh:
+        return json.load(fh)
+
+
+def dec(v):
+    """float.hex strings -> float, ints stay ints, None stays None."""
+    if isinstance(v, str):
+        return float.fromhex(v)
+    return v
+
+
+def dec_table(t):
+    return [[dec(x) for x in row] for row in t]
+
+
+def dec_input(inp):
+    return dec_table(inp["constraints"]), [dec(x) for x in inp["function"]]
+
+
+def table_hash(table) -> str:
+    h = hashlib.sha256()
+    for row in table:
+        h.update(struct.pack("<%dd" % len(row), *[float(x) for x in row]))
+    return h.hexdigest()
+
+
+def dense_hash(T: np.ndarray, n: int, flen: int) -> str:
+    """Hash of a dense tableau in the reference's ragged layout (f-row trimmed to flen)."""
+    h = hashlib.sha256()
+    T = np.ascontiguousarray(T, dtype="<f8")
+    h.update(T[:n].tobytes())
+    h.update(T[n, :flen].tobytes())
+    return h.hexdigest()
+
+
+def same_value(a, b, signed_zero=True) -> bool:
+    """Bitwise float equality (NaN == NaN; -0.0 != 0.0 unless signed_zero=False)."""
+    if isinstance(a, int) and isinstance(b, int):
+        return a == b
+    a, b = float(a), float(b)
+    if math.isnan(a) or math.isnan(b):
+        return math.isnan(a) and math.isnan(b)
+    if a == 0 and b == 0 and signed_zero:
+        return math.copysign(1, a) == math.copysign(1, b)
+    return a == b
+
+
+def same_table(t1, t2, signed_zero=True) -> bool:
+    if len(t1) != len(t2):
+        return False
+    for r1, r2 in zip(t1, t2):
+        if len(r1) != len(r2):
+            return False
+        if not all(same_value(a, b, signed_zero) for a, b in zip(r1, r2)):
+            return False
+    return True
+
+
+def all_int_input(cons, func) -> bool:
+    return all(isinstance(x, int) for r in cons for x in r) or all(isinstance(x, int) for x in func)
+
+
+def trajectory_cases():
+    """Every fixture that has a capped trajectory: yields (label, constraints, function, rec)."""
+    for k, rec in enumerate(load("random.json")):
+        yield f"random{k}_{rec['n']}x{rec['m']}", *dec_input(rec["input"]), rec
+    for k, rec in enumerate(load("ties.json")):
+        yield f"ties{k}", *dec_input(rec["input"]), rec
+    for k, rec in enumerate(load("degenerate.json")):
+        yield f"deg{k}_{rec['n']}x{rec['m']}", *dec_input(rec["input"]), rec
+    for name, rec in load("edge.json").items():
+        yield f"edge_{name}", *dec_input(rec["input"]), rec["solution"]["trajectory"]
+
+
+def trajectory_cap(rec) -> int:
+    """Pivots to run so a replay ends exactly where the fixture ended (terminal pick included)."""
+    pivots = len(rec["steps"]) - 1
+    return pivots if rec["outcome"]["kind"] == "cap" else pivots + 1
