@@ -1,0 +1,157 @@
+"""Benchmark: pivots/s and achieved HBM GB/s of the MI355X simplex pivot engine.
+
+Workload (BASELINE.json configs[3], the north-star target config): a 16384 x 16384 dense fp64
+tableau (n = m = 16383; seeded uniform random LP A~U(-1,1), b~U(0.1,1), c~U(-1,1), feasible at
+the origin so the trajectory is a long phase-2 run), resident in HBM before timing starts.
+A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): the selection
+kernel (pick_element, :70-141) + the fused update kernel (recalculate_matrix, :143-177).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--size S]
+
+N = 1: one process.  N > 1: launched by torch.distributed.run, one rank per GPU; the tableau's
+constraint rows are block-partitioned (strong scaling of the same tableau) and every pivot
+exchanges one all-gather of (header + candidate rows) over RCCL.  Timing: barrier +
+synchronize on both sides of exactly K pivots, max over ranks.  Rank 0 prints ONE JSON line.
+
+roofline: algorithmic bytes of the update kernel = 16 B per tableau element per pivot
+(read + write every element once), divided by that kernel's average duration measured with
+HIP events on the solver stream inside the timed region.  traffic: HBM bytes per launch from
+the committed rocprofv3 PMC summary (profiles/), FETCH_SIZE doubled per the gfx950 correction.
+cpu_baseline: the numpy restatement of the same pivot (oracle/numpy_oracle.py, bit-identical to
+the reference) on the same tableau, single thread, a bounded number of pivots.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "simplex-method-solver_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "pivots/sec + achieved HBM GB/s, dense fp64 tableau, 1/2/4/8 MI355X"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--size", type=int, default=16384, help="tableau is size x size (n=m=size-1)")
+    ap.add_argument("--kind", default="uniform")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=None, help="PMC summary json (default: profiles/)")
+    return ap.parse_args()
+
+
+def load_traffic(path, workload):
+    if path is None:
+        path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        rec = d.get(workload)
+        return None if rec is None else float(rec["bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(T, n, m, seconds):
+    """numpy port (oracle/numpy_oracle.py) timed on this host, 1 thread, bounded sample."""
+    import numpy as np
+    from oracle import numpy_oracle
+    A = np.ascontiguousarray(T)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        st, r, c = numpy_oracle.pick(A, n, m, m)
+        if st != numpy_oracle.PIVOT:
+            break
+        A = numpy_oracle.pivot(A, r, c)
+        done += 1
+        if time.perf_counter() - t0 >= seconds and done >= 2:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "pivots/s", "cores": 1, "kind": "port",
+            "sample": f"{done} pivots of the same {n + 1}x{m + 1} tableau from step 0 "
+                      f"(numpy restatement, single thread), {dt:.1f} s"}
+
+
+def run_single(args):
+    import numpy as np
+    import torch
+    from simplex_mi355x import lp
+    from simplex_mi355x.device import DeviceTableau
+
+    n = m = args.size - 1
+    R, C = n + 1, m + 1
+    T = lp.dense_tableau(args.kind, args.seed, n, m)
+    dev = DeviceTableau(T, n, m, m, device="cuda:0")
+    if args.warmup:
+        dev.run_timed(args.warmup)
+        dev.sync_state()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    upd_ms, dev_ms = dev.run_timed(args.steps)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ctl = dev.sync_state()
+    valid = int(ctl["npivots"]) == args.warmup + args.steps and not ctl["term"]
+    bytes_per_pivot = 16.0 * R * C
+    avg_upd = float(np.mean(upd_ms)) * 1e-3
+    achieved = bytes_per_pivot / avg_upd / 1e9
+    workload = f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
+    traffic = load_traffic(args.traffic, f"{R}x{C}")
+    out = {
+        "metric": METRIC,
+        "value": args.steps / wall,
+        "unit": "pivots/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: seeded dense random LP generated on the host, uploaded to HBM "
+                "before timing (no dataset)",
+        "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
+                   "parallelism": "single GPU", "kernels_per_pivot": 2},
+        "hbm_gbs_per_pivot": bytes_per_pivot / (wall / args.steps) / 1e9,
+        "device_ms_per_step": dev_ms / args.steps,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                     "kernel": "k_update<kSingle>",
+                     "algorithmic_bytes_per_launch": bytes_per_pivot,
+                     "avg_kernel_ms": avg_upd * 1e3},
+        "trajectory_valid": bool(valid),
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(T, n, m, args.cpu_seconds)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.gpus > 1:
+        from simplex_mi355x import sharded
+        sharded.bench_main(args, METRIC, PEAK_HBM_GBS, cpu_baseline, load_traffic)
+    else:
+        run_single(args)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+/*
+ * smx.h -- C ABI of the MI355X simplex pivot engine (libsmx.so, gfx950).
+ *
+ * Drop-in boundary for the hot path of jqnfxa/Simplex-Method-Solver, src/simplex.py:
+ *   smx_reset      <- the tableau set-up of SimplexMethod.__init__ (simplex.py:25-39): primes
+ *                     the device control block with the first-negative "-b" row and the first
+ *                     negative f-row column of a freshly uploaded tableau
+ *   smx_select     <- SimplexMethod.pick_element (simplex.py:70-141), per-workgroup partials
+ *   smx_finalize   <- the return/raise of pick_element (simplex.py:89, 91, 101-103, 138-141)
+ *   smx_update     <- SimplexMethod.recalculate_matrix (simplex.py:143-177), steps 1-4,
+ *                     out of place like the reference's deepcopy (simplex.py:149, 177)
+ *   smx_run        <- the pivot loop of SimplexMethod.get_solution (simplex.py:184-198),
+ *                     k chained select+update pairs, no host synchronisation
+ *   smx_graph_*    <- the same loop captured once as a hipGraph and replayed
+ *   smx_shard_*    <- row-sharded variant for 1 process per GPU (exchange done by the caller's
+ *                     RCCL all-gather between smx_shard_pack and smx_shard_merge)
+ * The reference is pure Python; it has no FFI of its own.  The Python binding a maintainer would
+ * add is in INTEGRATION.md (ctypes), and simplex-method-solver_amd/simplex_mi355x/_lib.py is it.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers owned by the caller (torch tensors in the Python host),
+ *     except where a name says host.  Every call is asynchronous on `stream` (a hipStream_t).
+ *   - Tableau: row-major fp64, R = n+1 rows (n constraint rows, then the f-row), C = m+1 used
+ *     columns (m variables, then the "-b" column), leading dimension `ld` (even, >= C+1 when C is
+ *     odd).  f-row entries j >= flen are padding: computed, never read by a selection.
+ *   - Two tableau buffers ping-pong: step s reads buf[s & 1] and writes buf[(s + 1) & 1];
+ *     `parity` = s & 1 selects the control-block slots of that step.
+ *   - Return value: 0 on success, otherwise a hipError_t (no exceptions cross this ABI).
+ *     The pivot outcome is device-side in smx_ctl.sel_status (SMX_* codes below), mapped by the
+ *     host to the reference's ValueError strings (simplex.py:89, 139).
+ */
+#ifndef SMX_H
+#define SMX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* outcome codes (also used by oracle/) */
+#define SMX_PIVOT 0         /* (r, c) selected; simplex.py:91, 141                          */
+#define SMX_OPTIMUM 1       /* no negative f-row coefficient; simplex.py:101-103             */
+#define SMX_INCORRECT 2     /* ValueError("incorrect system"); simplex.py:88-89              */
+#define SMX_NOT_CONVERGE 3  /* ValueError("simplex method does not converge"); :138-139      */
+#define SMX_FSHORT 4        /* len(function) < m and the f-row scan ran off its end (IndexError) */
+#define SMX_IDLE 5          /* no selection made yet                                         */
+
+#define SMX_NONE 0x7f7f7f7f /* "no index" sentinel (memset byte 0x7f)                        */
+
+/* Device control block (caller allocates sizeof(smx_ctl) bytes of device memory). */
+typedef struct smx_ctl {
+    int32_t negb[2];    /* per parity slot: first row i < n with T[i][m] < 0 (global index)  */
+    int32_t negf[2];    /* per parity slot: first j < min(m, flen) with f[j] < 0             */
+    int32_t term;       /* != 0: a terminal outcome was reached; chained kernels do nothing  */
+    int32_t sel_status; /* last selection: SMX_* code                                         */
+    int32_t sel_r;      /* last selection: pivot row (global)                                 */
+    int32_t sel_c;      /* last selection: pivot column                                       */
+    double sel_e;       /* last selection: pivot element T[r][c]                              */
+    int64_t npivots;    /* pivots applied since smx_reset(..., clear_count=1)                 */
+    int32_t sel_owner;  /* sharded: rank whose candidate row is the pivot row                 */
+    int32_t pad0;
+    int64_t reserved[9];    /* reserved[0]: sharded, offset (in doubles) of the pivot row in recv */
+} smx_ctl; /* 128 bytes */
+
+/* One per select workgroup (caller allocates nparts * sizeof(smx_part) bytes). */
+typedef struct smx_part {
+    int32_t p1col;    /* phase 1: first column j with T[r][j] > 0 in this workgroup's slice  */
+    int32_t first;    /* phase 2: first row with T[i][c] != 0 (its ratio may be NaN)         */
+    double first_v;   /* ratio T[first][m] / T[first][c]                                     */
+    int32_t best_cls; /* best non-NaN candidate: 0 (v<0), 1 (v==0), 2 (v>0), 3 none          */
+    int32_t best_i;
+    double best_v;
+} smx_part; /* 32 bytes */
+
+/* Shape of one (possibly sharded) tableau. */
+typedef struct smx_shape {
+    int64_t ld;     /* leading dimension in doubles                                         */
+    int32_t rows;   /* local constraint rows (n when unsharded)                              */
+    int32_t n;      /* global constraint rows                                                */
+    int32_t m;      /* variables                                                             */
+    int32_t flen;   /* len(function) of the reference's f-row                                */
+    int32_t row0;   /* global index of local row 0 (0 when unsharded)                        */
+    int32_t nparts; /* select workgroups (smx_part records)                                  */
+} smx_shape;
+
+/* Library/ABI identification; returns the number of kernels built into the library. */
+int smx_version(char* buf, int len);
+/* Recommended number of select partials for a shape (host-only helper). */
+int smx_nparts_for(int32_t rows, int32_t m);
+
+/* Scan a freshly uploaded tableau into ctl slot `parity`; clears term, sets sel_status = IDLE,
+ * and zeroes npivots when clear_count != 0. */
+int smx_reset(const double* T, const smx_shape* shape, int32_t parity, int32_t clear_count,
+              smx_ctl* ctl, void* stream);
+
+/* pick_element, part 1: per-workgroup partials of the selection for the tableau T. */
+int smx_select(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+               smx_part* parts, void* stream);
+
+/* pick_element, part 2: reduce the partials into ctl->sel_* (does not set term, logs nothing). */
+int smx_finalize(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                 const smx_part* parts, void* stream);
+
+/* recalculate_matrix: reduce the partials, record the outcome in ctl (sel_*, term, npivots,
+ * log[npivots % log_cap] = (r, c)), and on SMX_PIVOT write the pivoted tableau to Tout.
+ * Also primes ctl slot parity^1 for the next step (fused first-negative scans). */
+int smx_update(const double* Tin, double* Tout, const smx_shape* shape, int32_t parity,
+               smx_ctl* ctl, const smx_part* parts, int32_t* log, int64_t log_cap,
+               void* stream);
+
+/* k pivots (select + update each), buffers buf0/buf1, first step's parity `parity`. */
+int smx_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+            smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream);
+
+/* The same k-pivot chain captured as a hipGraph (opaque handle); replay with smx_graph_launch. */
+int smx_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                     int32_t k, smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap,
+                     void* stream, void** graph_out);
+int smx_graph_launch(void* graph, void* stream);
+int smx_graph_destroy(void* graph);
+
+/* smx_run with HIP events recorded on `stream` around every update kernel; synchronises, then
+ * writes each update kernel's duration (ms) to host_update_ms[0..k-1] and the whole chain's
+ * device time (first select start -> last update end) to *host_total_ms. */
+int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                  smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream,
+                  float* host_update_ms, float* host_total_ms);
+
+/* Forced-pivot microbenchmark of the update kernel alone: applies pivot (r, c) from Tin to Tout
+ * without any selection (used to measure the kernel against the HBM roofline). */
+int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, int32_t r,
+                      int32_t c, void* stream);
+
+/* ---- row-sharded engine (one process per GPU; exchange = caller's all-gather) ----------
+ * Local tableau: shape->rows constraint rows (global rows row0 .. row0+rows-1) + a replica
+ * of the f-row as local row `rows`.  Per pivot:
+ *   smx_select(T, shape, parity, ...)            local ratio-test partials
+ *   smx_shard_pack(T, ..., send)                 header + candidate row -> send[hdr + ld]
+ *   all_gather(send -> recv[P][hdr + ld])        RCCL over xGMI, by the caller
+ *   smx_shard_merge(recv, P, ...)                identical decision on every rank -> ctl
+ *   smx_shard_update(Tin, Tout, recv, ...)       pivot with the winning row
+ * SMX_SHARD_HDR doubles of header precede the row in each send/recv slot. */
+#define SMX_SHARD_HDR 8
+int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
+                   const smx_part* parts, double* send, void* stream);
+int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,
+                    int32_t parity, smx_ctl* ctl, int32_t* log, int64_t log_cap, void* stream);
+int smx_shard_update(const double* Tin, double* Tout, const double* recv,
+                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMX_H */

@@ -1,0 +1,878 @@
+// smx_kernels.hip -- CDNA4 (gfx950) kernels of the simplex pivot engine + the C ABI of smx.h.
+//
+// Hot path of jqnfxa/Simplex-Method-Solver src/simplex.py, re-designed for MI355X:
+//   k_select  : pick_element partials (simplex.py:70-141), one record per workgroup
+//   k_finalize: pick_element outcome (simplex.py:89, 91, 101-103, 138-141)
+//   k_update  : recalculate_matrix (simplex.py:143-177) fused with the decision (every block
+//               reduces the select partials itself: no extra launch, no inter-block protocol)
+//               and with the NEXT step's first-negative scans of the "-b" column and f-row
+//   k_reset   : first-negative scans of a freshly uploaded tableau (set-up, simplex.py:25-39)
+//   k_pack / k_merge / k_update<SHARD> : the row-sharded variant (one rank per GPU)
+//
+// Arithmetic parity: every element is (t*e - pr*pc)/e with each op rounded on its own, exactly
+// as CPython evaluates simplex.py:173-175.  This file is compiled with -ffp-contract=off and
+// additionally pins `#pragma clang fp contract(off)`; fp64 division is the IEEE-correct
+// div_scale/rcp/fma/div_fmas/div_fixup sequence (never a reciprocal multiply).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "smx.h"
+
+#pragma clang fp contract(off)
+
+static_assert(sizeof(smx_ctl) == 128, "smx_ctl layout");
+static_assert(sizeof(smx_part) == 32, "smx_part layout");
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kSelBlock = 256;
+constexpr int kUpdBlock = 256;
+constexpr int kUpdWaves = kUpdBlock / kWave;
+constexpr int kRowsPerTile = 8;      // rows per wave work unit (8 x 16 B loads in flight/lane)
+constexpr int kMaxUpdGrid = 2048;    // 256 CUs x 8 resident blocks; grid-stride beyond
+constexpr int kMaxParts = 64;
+
+// ---------------------------------------------------------------------------------------------
+// Ratio-test candidate order (simplex.py:105-141 restated as an arg-min, see oracle/numpy_oracle):
+// class 0: v < 0, larger v better, ties -> larger row; class 1: v == 0 (incl. -0.0), smaller row;
+// class 2: v > 0, smaller row; class 3: no candidate.  NaN ratios never enter this order.
+struct Cand {
+    int cls;
+    int idx;
+    double v;
+};
+
+__device__ __forceinline__ Cand cand_none() { return Cand{3, SMX_NONE, 0.0}; }
+
+__device__ __forceinline__ Cand classify(double v, int idx) {
+    Cand c;
+    c.cls = (v < 0.0) ? 0 : ((v == 0.0) ? 1 : 2);
+    c.idx = idx;
+    c.v = v;
+    return c;
+}
+
+__device__ __forceinline__ bool better(const Cand& a, const Cand& b) {
+    if (a.cls != b.cls) return a.cls < b.cls;
+    if (a.cls == 0) return (a.v > b.v) || (a.v == b.v && a.idx > b.idx);
+    return a.idx < b.idx;
+}
+
+__device__ __forceinline__ Cand shfl_xor_cand(const Cand& a, int mask) {
+    Cand o;
+    o.cls = __shfl_xor(a.cls, mask, kWave);
+    o.idx = __shfl_xor(a.idx, mask, kWave);
+    o.v = __shfl_xor(a.v, mask, kWave);
+    return o;
+}
+
+// "first candidate" = smallest row with T[i][c] != 0, carrying its (possibly NaN) ratio
+struct First {
+    int idx;
+    double v;
+};
+
+__device__ __forceinline__ First shfl_xor_first(const First& a, int mask) {
+    First o;
+    o.idx = __shfl_xor(a.idx, mask, kWave);
+    o.v = __shfl_xor(a.v, mask, kWave);
+    return o;
+}
+
+__device__ __forceinline__ int wave_min_int(int x) {
+#pragma unroll
+    for (int mask = 32; mask >= 1; mask >>= 1) x = min(x, __shfl_xor(x, mask, kWave));
+    return x;
+}
+
+__device__ __forceinline__ Cand wave_best(Cand a) {
+#pragma unroll
+    for (int mask = 32; mask >= 1; mask >>= 1) {
+        Cand o = shfl_xor_cand(a, mask);
+        if (better(o, a)) a = o;
+    }
+    return a;
+}
+
+__device__ __forceinline__ First wave_first(First a) {
+#pragma unroll
+    for (int mask = 32; mask >= 1; mask >>= 1) {
+        First o = shfl_xor_first(a, mask);
+        if (o.idx < a.idx) a = o;
+    }
+    return a;
+}
+
+struct Decision {
+    int status;
+    int r;
+    int c;
+};
+
+// The outcome of pick_element from the select partials (run by one wave; lanes cover parts).
+// simplex.py:72-91 (phase 1), :94-103 (entering column / optimum), :105-141 (leaving row).
+__device__ Decision decide_from_parts(const smx_ctl* ctl, const smx_part* parts, int nparts,
+                                      int parity, int n, int m, int flen) {
+    const int lane = threadIdx.x & (kWave - 1);
+    Decision d;
+    const int negb = ctl->negb[parity];
+    if (negb != SMX_NONE && negb < n) {
+        int p1 = SMX_NONE;
+        for (int k = lane; k < nparts; k += kWave) p1 = min(p1, parts[k].p1col);
+        p1 = wave_min_int(p1);
+        d.r = negb;
+        d.c = p1;
+        d.status = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
+        return d;
+    }
+    const int c = ctl->negf[parity];
+    d.c = c;
+    d.r = SMX_NONE;
+    if (c == SMX_NONE) {
+        d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
+        return d;
+    }
+    First f{SMX_NONE, 0.0};
+    Cand b = cand_none();
+    for (int k = lane; k < nparts; k += kWave) {
+        const smx_part p = parts[k];
+        if (p.first < f.idx) {
+            f.idx = p.first;
+            f.v = p.first_v;
+        }
+        Cand o{p.best_cls, p.best_i, p.best_v};
+        if (better(o, b)) b = o;
+    }
+    f = wave_first(f);
+    b = wave_best(b);
+    if (f.idx == SMX_NONE) {
+        d.status = SMX_NOT_CONVERGE;              // first_try still set (simplex.py:138)
+    } else if (isnan(f.v)) {
+        d.status = SMX_PIVOT;                     // a NaN first candidate sticks (:117-121)
+        d.r = f.idx;
+    } else if (b.cls >= 2) {
+        d.status = SMX_NOT_CONVERGE;              // min_val > 0 (simplex.py:138-139)
+    } else {
+        d.status = SMX_PIVOT;
+        d.r = b.idx;
+    }
+    return d;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_reset: scan the "-b" column (rows < rows_local) and the f-row (j < fscan) of a tableau.
+__global__ __launch_bounds__(1024) void k_reset(const double* __restrict__ T, int64_t ld,
+                                                int rows, int m, int fscan, int row0,
+                                                int parity, int clear_count,
+                                                smx_ctl* __restrict__ ctl) {
+    __shared__ int s_b[16], s_f[16];
+    const int tid = threadIdx.x;
+    int nb = SMX_NONE, nf = SMX_NONE;
+    for (int i = tid; i < rows; i += blockDim.x) {
+        if (T[(int64_t)i * ld + m] < 0.0) {
+            nb = row0 + i;
+            break;
+        }
+    }
+    const double* f = T + (int64_t)rows * ld;
+    for (int j = tid; j < fscan; j += blockDim.x) {
+        if (f[j] < 0.0) {
+            nf = j;
+            break;
+        }
+    }
+    nb = wave_min_int(nb);
+    nf = wave_min_int(nf);
+    if ((tid & 63) == 0) {
+        s_b[tid >> 6] = nb;
+        s_f[tid >> 6] = nf;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            nb = min(nb, s_b[w]);
+            nf = min(nf, s_f[w]);
+        }
+        ctl->negb[parity] = nb;
+        ctl->negf[parity] = nf;
+        ctl->negb[parity ^ 1] = SMX_NONE;
+        ctl->negf[parity ^ 1] = SMX_NONE;
+        ctl->term = 0;
+        ctl->sel_status = SMX_IDLE;
+        ctl->sel_r = SMX_NONE;
+        ctl->sel_c = SMX_NONE;
+        if (clear_count) ctl->npivots = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_select: per-workgroup partials of pick_element.  Phase 1: first positive entry of the
+// first-negative-b row, sliced over columns.  Phase 2: first candidate + best non-NaN key of the
+// ratio test over the entering column, sliced over rows (two strided loads per row, spread over
+// many CUs so the gather is not limited by one CU's fabric bandwidth).
+__global__ __launch_bounds__(kSelBlock) void k_select(const double* __restrict__ T, int64_t ld,
+                                                      int rows, int m, int row0, int parity,
+                                                      smx_ctl* __restrict__ ctl,
+                                                      smx_part* __restrict__ parts) {
+    __shared__ int s_i[kSelBlock / kWave];
+    __shared__ First s_f[kSelBlock / kWave];
+    __shared__ Cand s_c[kSelBlock / kWave];
+    const int tid = threadIdx.x;
+    const int wid = tid >> 6;
+    if (ctl->term) return;
+    if (blockIdx.x == 0 && tid == 0) {
+        // the slot the update of this step fills for the next step (it atomically min-s into it)
+        ctl->negb[parity ^ 1] = SMX_NONE;
+        ctl->negf[parity ^ 1] = SMX_NONE;
+    }
+    const int gtid = blockIdx.x * kSelBlock + tid;
+    const int gstride = gridDim.x * kSelBlock;
+    const int negb = ctl->negb[parity];
+    if (negb != SMX_NONE && negb >= row0 && negb < row0 + rows) {
+        // phase 1 (simplex.py:81-85): first j < m with T[r][j] > 0
+        const double* rowp = T + (int64_t)(negb - row0) * ld;
+        int p1 = SMX_NONE;
+        for (int j = gtid; j < m; j += gstride) {
+            if (rowp[j] > 0.0) {
+                p1 = j;
+                break;
+            }
+        }
+        p1 = wave_min_int(p1);
+        if ((tid & 63) == 0) s_i[wid] = p1;
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < kSelBlock / kWave; ++w) p1 = min(p1, s_i[w]);
+            parts[blockIdx.x].p1col = p1;
+        }
+        return;
+    }
+    const int c = ctl->negf[parity];
+    if (c == SMX_NONE) return;
+    // phase 2 ratio test (simplex.py:111-136)
+    First f{SMX_NONE, 0.0};
+    Cand b = cand_none();
+    for (int i = gtid; i < rows; i += gstride) {
+        const double* rowp = T + (int64_t)i * ld;
+        const double a = rowp[c];
+        const double bb = rowp[m];
+        if (a != 0.0) {                                  // simplex.py:112 (NaN counts)
+            const double v = bb / a;                     // simplex.py:115
+            const int gi = row0 + i;
+            if (gi < f.idx) {
+                f.idx = gi;
+                f.v = v;
+            }
+            if (!isnan(v)) {
+                const Cand x = classify(v, gi);
+                if (better(x, b)) b = x;
+            }
+        }
+    }
+    f = wave_first(f);
+    b = wave_best(b);
+    if ((tid & 63) == 0) {
+        s_f[wid] = f;
+        s_c[wid] = b;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < kSelBlock / kWave; ++w) {
+            if (s_f[w].idx < f.idx) f = s_f[w];
+            if (better(s_c[w], b)) b = s_c[w];
+        }
+        smx_part p;
+        p.p1col = SMX_NONE;
+        p.first = f.idx;
+        p.first_v = f.v;
+        p.best_cls = b.cls;
+        p.best_i = b.idx;
+        p.best_v = b.v;
+        parts[blockIdx.x] = p;
+    }
+}
+
+__global__ __launch_bounds__(kWave) void k_finalize(const smx_part* __restrict__ parts,
+                                                    int nparts, int parity, int n, int m,
+                                                    int flen, const double* __restrict__ T,
+                                                    int64_t ld, smx_ctl* __restrict__ ctl) {
+    const Decision d = decide_from_parts(ctl, parts, nparts, parity, n, m, flen);
+    if (threadIdx.x == 0) {
+        ctl->sel_status = d.status;
+        ctl->sel_r = d.r;
+        ctl->sel_c = d.c;
+        ctl->sel_e = (d.status == SMX_PIVOT) ? T[(int64_t)d.r * ld + d.c] : 0.0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_update: the modified Jordan step (simplex.py:149-177), out of place.
+//
+// Work unit = one wave x kRowsPerTile rows x 64 lanes x 2 doubles (a 1 KiB column chunk per
+// row): per row one 16-B load + one 16-B store per lane, the pivot-row chunk held in registers
+// for all rows of the unit, T[i][c] a wave-uniform scalar load.  Per element:
+//     num = (i == r) ? (j == c ? 1.0 : -x)          steps 1 and 3
+//                    : (j == c ? x   : x*e - pr*pc) steps 2 and 4
+//     out = num / e
+// which is exactly the value the reference leaves in new_table[i][j] after steps 1-4.
+enum UpdMode { kSingle = 0, kShard = 1, kForced = 2 };
+
+template <int MODE>
+__global__ __launch_bounds__(kUpdBlock) void k_update(
+    const double* __restrict__ Tin, double* __restrict__ Tout, int64_t ld, int rows_local,
+    int n, int m, int flen, int fscan, int row0, int parity, smx_ctl* __restrict__ ctl,
+    const smx_part* __restrict__ parts, int nparts, int32_t* __restrict__ log, int64_t log_cap,
+    const double* __restrict__ recv, int forced_r, int forced_c) {
+    __shared__ int s_dec[3];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    int r, c;
+    const double* prow;
+    if (MODE == kForced) {
+        r = forced_r;
+        c = forced_c;
+        prow = Tin + (int64_t)r * ld;
+    } else {
+        if (ctl->term) return;
+        if (MODE == kSingle) {
+            if (tid < kWave) {
+                const Decision d = decide_from_parts(ctl, parts, nparts, parity, n, m, flen);
+                if (tid == 0) {
+                    s_dec[0] = d.status;
+                    s_dec[1] = d.r;
+                    s_dec[2] = d.c;
+                    if (blockIdx.x == 0) {
+                        ctl->sel_status = d.status;
+                        ctl->sel_r = d.r;
+                        ctl->sel_c = d.c;
+                        if (d.status == SMX_PIVOT) {
+                            ctl->sel_e = Tin[(int64_t)d.r * ld + d.c];
+                            const int64_t k = ctl->npivots;
+                            if (log_cap > 0) {
+                                log[2 * (k % log_cap)] = d.r;
+                                log[2 * (k % log_cap) + 1] = d.c;
+                            }
+                            ctl->npivots = k + 1;
+                        } else {
+                            ctl->term = 1;
+                        }
+                    }
+                }
+            }
+            __syncthreads();
+            if (s_dec[0] != SMX_PIVOT) return;
+            r = __builtin_amdgcn_readfirstlane(s_dec[1]);
+            c = __builtin_amdgcn_readfirstlane(s_dec[2]);
+            prow = Tin + (int64_t)r * ld;
+        } else {  // kShard: k_merge already decided and published into ctl
+            if (ctl->sel_status != SMX_PIVOT) return;
+            r = __builtin_amdgcn_readfirstlane(ctl->sel_r);
+            c = __builtin_amdgcn_readfirstlane(ctl->sel_c);
+            const int64_t off = ctl->reserved[0];
+            prow = recv + off;
+        }
+    }
+    const double e = prow[c];
+    const int r_local = r - row0;  // may be outside [0, rows_local): pivot row lives elsewhere
+    const int R = rows_local + 1;  // + the f-row (local row rows_local)
+    const int C = m + 1;
+    const int vpr = (C + 1) >> 1;                     // 2-double vectors per row
+    const int nchunks = (vpr + kWave - 1) / kWave;    // 64-vector chunks per row
+    const int rtiles = (R + kRowsPerTile - 1) / kRowsPerTile;
+    const int64_t units = (int64_t)nchunks * rtiles;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int negslot = parity ^ 1;
+    int lb = SMX_NONE;   // fused next-step scan: first row with new b < 0 (this lane)
+    int lf = SMX_NONE;   // fused next-step scan: first f-row column with new f < 0 (this lane)
+
+    for (int64_t u = (int64_t)blockIdx.x * kUpdWaves + wid; u < units;
+         u += (int64_t)gridDim.x * kUpdWaves) {
+        const int ch = (int)(u % nchunks);
+        const int i0 = (int)(u / nchunks) * kRowsPerTile;
+        const int v = ch * kWave + lane;
+        const bool active = v < vpr;
+        const int j = 2 * v;
+        double2 pr = make_double2(0.0, 0.0);
+        if (active) pr = *reinterpret_cast<const double2*>(prow + j);
+        double2 x[kRowsPerTile];
+        double pc[kRowsPerTile];
+#pragma unroll
+        for (int k = 0; k < kRowsPerTile; ++k) {
+            const int i = i0 + k;
+            pc[k] = 0.0;
+            x[k] = make_double2(0.0, 0.0);
+            if (i < R) {
+                const double* src = Tin + (int64_t)i * ld;
+                pc[k] = src[c];
+                if (active) x[k] = *reinterpret_cast<const double2*>(src + j);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kRowsPerTile; ++k) {
+            const int i = i0 + k;
+            if (i >= R) break;
+            double n0, n1;
+            if (i == r_local) {
+                n0 = (j == c) ? 1.0 : -x[k].x;
+                n1 = (j + 1 == c) ? 1.0 : -x[k].y;
+            } else {
+                const double a0 = x[k].x * e;
+                const double b0 = pr.x * pc[k];
+                const double a1 = x[k].y * e;
+                const double b1 = pr.y * pc[k];
+                n0 = (j == c) ? x[k].x : (a0 - b0);
+                n1 = (j + 1 == c) ? x[k].y : (a1 - b1);
+            }
+            double2 o;
+            o.x = n0 / e;
+            o.y = n1 / e;
+            if (active) {
+                *reinterpret_cast<double2*>(Tout + (int64_t)i * ld + j) = o;
+                if (MODE != kForced) {
+                    if (i < rows_local) {
+                        const double nb = (j == m) ? o.x : o.y;
+                        if ((j == m || j + 1 == m) && nb < 0.0) lb = min(lb, row0 + i);
+                    } else {
+                        if (j < fscan && o.x < 0.0) lf = min(lf, j);
+                        if (j + 1 < fscan && o.y < 0.0) lf = min(lf, j + 1);
+                    }
+                }
+            }
+        }
+    }
+    if (MODE != kForced) {
+        lb = wave_min_int(lb);
+        lf = wave_min_int(lf);
+        if (lane == 0) {
+            if (lb != SMX_NONE) atomicMin(&ctl->negb[negslot], lb);
+            if (lf != SMX_NONE) atomicMin(&ctl->negf[negslot], lf);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sharded exchange.  Send slot layout (doubles): [hdr SMX_SHARD_HDR][row A: ld][row B: ld]
+//   hdr[0] local first-negative-b row (global) or NONE      -> row B = that row (phase 1)
+//   hdr[1] first ratio candidate row (global) or NONE        -> row A = that row if its v is NaN
+//   hdr[2] its ratio v
+//   hdr[3] best class, hdr[4] best row (global), hdr[5] best v -> row B = best row (phase 2)
+//   hdr[6] entering column c (replicated f-row => same on every rank)
+__global__ __launch_bounds__(kUpdBlock) void k_pack(const double* __restrict__ T, int64_t ld,
+                                                     int rows, int m, int row0, int parity,
+                                                     const smx_ctl* __restrict__ ctl,
+                                                     const smx_part* __restrict__ parts,
+                                                     int nparts, double* __restrict__ send) {
+    __shared__ int s_rows[2];
+    __shared__ int s_hdr_i[4];
+    __shared__ double s_hdr_d[2];
+    const int tid = threadIdx.x;
+    if (ctl->term) return;
+    if (tid < kWave) {
+        const int negb = ctl->negb[parity];
+        const int c = ctl->negf[parity];
+        First f{SMX_NONE, 0.0};
+        Cand b = cand_none();
+        if (negb == SMX_NONE && c != SMX_NONE) {
+            for (int k = tid; k < nparts; k += kWave) {
+                const smx_part p = parts[k];
+                if (p.first < f.idx) {
+                    f.idx = p.first;
+                    f.v = p.first_v;
+                }
+                Cand o{p.best_cls, p.best_i, p.best_v};
+                if (better(o, b)) b = o;
+            }
+            f = wave_first(f);
+            b = wave_best(b);
+        }
+        if (tid == 0) {
+            s_rows[0] = (f.idx != SMX_NONE && isnan(f.v)) ? f.idx - row0 : -1;     // row A
+            s_rows[1] = (negb != SMX_NONE) ? negb - row0 : (b.cls < 3 ? b.idx - row0 : -1);
+            s_hdr_i[0] = negb;
+            s_hdr_i[1] = f.idx;
+            s_hdr_i[2] = b.cls;
+            s_hdr_i[3] = b.idx;
+            s_hdr_d[0] = f.v;
+            s_hdr_d[1] = b.v;
+            if (blockIdx.x == 0) {
+                send[0] = (double)negb;
+                send[1] = (double)f.idx;
+                send[2] = f.v;
+                send[3] = (double)b.cls;
+                send[4] = (double)b.idx;
+                send[5] = b.v;
+                send[6] = (double)c;
+                send[7] = 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    const int ra = s_rows[0], rb = s_rows[1];
+    const int C = m + 1;
+    const int gt = blockIdx.x * kUpdBlock + tid;
+    const int gs = gridDim.x * kUpdBlock;
+    for (int j = gt; j < C + 1 && j < ld; j += gs) {
+        if (ra >= 0) send[SMX_SHARD_HDR + j] = T[(int64_t)ra * ld + j];
+        if (rb >= 0) send[SMX_SHARD_HDR + ld + j] = T[(int64_t)rb * ld + j];
+    }
+}
+
+// Every rank merges the P headers identically (one workgroup) and, in phase 1, scans the
+// winning row for its first positive entry (simplex.py:81-85).
+__global__ __launch_bounds__(1024) void k_merge(const double* __restrict__ recv, int nranks,
+                                                int64_t ld, int n, int m, int flen,
+                                                smx_ctl* __restrict__ ctl,
+                                                int32_t* __restrict__ log, int64_t log_cap) {
+    __shared__ int s_dec[4];
+    __shared__ int64_t s_off;
+    __shared__ int s_w[16];
+    const int tid = threadIdx.x;
+    const int64_t slot = SMX_SHARD_HDR + 2 * ld;
+    if (ctl->term) return;
+    if (tid == 0) {
+        int gnegb = SMX_NONE, owner_b = -1;
+        int gfirst = SMX_NONE, owner_f = -1;
+        double fv = 0.0;
+        Cand best = cand_none();
+        int owner_best = -1;
+        int c = SMX_NONE;
+        for (int p = 0; p < nranks; ++p) {
+            const double* h = recv + p * slot;
+            const int nb = (int)h[0];
+            if (nb < gnegb) {
+                gnegb = nb;
+                owner_b = p;
+            }
+            const int fi = (int)h[1];
+            if (fi < gfirst) {
+                gfirst = fi;
+                fv = h[2];
+                owner_f = p;
+            }
+            Cand o{(int)h[3], (int)h[4], h[5]};
+            if (better(o, best)) {
+                best = o;
+                owner_best = p;
+            }
+            c = (int)h[6];
+        }
+        int status, r = SMX_NONE;
+        int64_t off = 0;
+        if (gnegb != SMX_NONE) {
+            status = -1;  // phase 1: column chosen below
+            r = gnegb;
+            off = owner_b * slot + SMX_SHARD_HDR + ld;
+        } else if (c == SMX_NONE) {
+            status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
+        } else if (gfirst == SMX_NONE) {
+            status = SMX_NOT_CONVERGE;
+        } else if (isnan(fv)) {
+            status = SMX_PIVOT;
+            r = gfirst;
+            off = owner_f * slot + SMX_SHARD_HDR;
+        } else if (best.cls >= 2) {
+            status = SMX_NOT_CONVERGE;
+        } else {
+            status = SMX_PIVOT;
+            r = best.idx;
+            off = owner_best * slot + SMX_SHARD_HDR + ld;
+        }
+        s_dec[0] = status;
+        s_dec[1] = r;
+        s_dec[2] = c;
+        s_dec[3] = (gnegb != SMX_NONE) ? owner_b : (status == SMX_PIVOT ? (int)(off / slot) : -1);
+        s_off = off;
+    }
+    __syncthreads();
+    int status = s_dec[0];
+    int c = s_dec[2];
+    if (status == -1) {
+        const double* prow = recv + s_off;
+        int p1 = SMX_NONE;
+        for (int j = tid; j < m; j += blockDim.x) {
+            if (prow[j] > 0.0) {
+                p1 = j;
+                break;
+            }
+        }
+        p1 = wave_min_int(p1);
+        if ((tid & 63) == 0) s_w[tid >> 6] = p1;
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < (int)(blockDim.x >> 6); ++w) p1 = min(p1, s_w[w]);
+            s_dec[0] = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
+            s_dec[2] = p1;
+        }
+        __syncthreads();
+        status = s_dec[0];
+        c = s_dec[2];
+    }
+    if (tid == 0) {
+        const int r = s_dec[1];
+        ctl->sel_status = status;
+        ctl->sel_r = r;
+        ctl->sel_c = c;
+        ctl->sel_owner = s_dec[3];
+        ctl->reserved[0] = s_off;
+        if (status == SMX_PIVOT) {
+            ctl->sel_e = recv[s_off + c];
+            const int64_t k = ctl->npivots;
+            if (log_cap > 0) {
+                log[2 * (k % log_cap)] = r;
+                log[2 * (k % log_cap) + 1] = c;
+            }
+            ctl->npivots = k + 1;
+        } else {
+            ctl->term = 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+inline int nparts_for(int rows, int m) {
+    const int work = rows > m ? rows : m;
+    int p = (work + kSelBlock - 1) / kSelBlock;
+    if (p < 1) p = 1;
+    if (p > kMaxParts) p = kMaxParts;
+    return p;
+}
+
+inline int update_grid(const smx_shape& s) {
+    const int R = s.rows + 1;
+    const int vpr = (s.m + 2) >> 1;
+    const int64_t nchunks = (vpr + kWave - 1) / kWave;
+    const int64_t units = nchunks * ((R + kRowsPerTile - 1) / kRowsPerTile);
+    int64_t blocks = (units + kUpdWaves - 1) / kUpdWaves;
+    if (blocks > kMaxUpdGrid) blocks = kMaxUpdGrid;
+    if (blocks < 1) blocks = 1;
+    return (int)blocks;
+}
+
+inline int fscan_of(const smx_shape& s) { return s.flen < s.m ? s.flen : s.m; }
+
+inline bool shape_ok(const smx_shape* s) {
+    if (!s) return false;
+    if (s->m < 0 || s->rows < 0 || s->n < s->rows || s->ld < s->m + 1) return false;
+    if ((s->ld & 1) != 0) return false;                   // 16-B aligned double2 rows
+    if (((s->m + 1) & 1) && s->ld < s->m + 2) return false;  // odd C: vector tail in padding
+    if (s->nparts < 1 || s->nparts > kMaxParts) return false;
+    return true;
+}
+
+inline hipStream_t S(void* p) { return reinterpret_cast<hipStream_t>(p); }
+
+int launch_select(const double* T, const smx_shape& s, int parity, smx_ctl* ctl, smx_part* parts,
+                  hipStream_t st) {
+    hipLaunchKernelGGL(k_select, dim3(s.nparts), dim3(kSelBlock), 0, st, T, s.ld, s.rows, s.m,
+                       s.row0, parity, ctl, parts);
+    return (int)hipGetLastError();
+}
+
+int launch_update(const double* Tin, double* Tout, const smx_shape& s, int parity, smx_ctl* ctl,
+                  const smx_part* parts, int32_t* log, int64_t log_cap, hipStream_t st) {
+    hipLaunchKernelGGL(k_update<kSingle>, dim3(update_grid(s)), dim3(kUpdBlock), 0, st, Tin, Tout,
+                       s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl, parts,
+                       s.nparts, log, log_cap, (const double*)nullptr, 0, 0);
+    return (int)hipGetLastError();
+}
+
+int launch_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, smx_ctl* ctl,
+                 smx_part* parts, int32_t* log, int64_t log_cap, hipStream_t st) {
+    for (int step = 0; step < k; ++step) {
+        const int p = (parity + step) & 1;
+        double* tin = p ? buf1 : buf0;
+        double* tout = p ? buf0 : buf1;
+        int err = launch_select(tin, s, p, ctl, parts, st);
+        if (err) return err;
+        err = launch_update(tin, tout, s, p, ctl, parts, log, log_cap, st);
+        if (err) return err;
+    }
+    return 0;
+}
+
+struct Graph {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+};
+
+}  // namespace
+
+// =============================================================================================
+extern "C" {
+
+int smx_version(char* buf, int len) {
+    const char* v = "smx 0.1 gfx950 fp64 (select, finalize, update<single|shard|forced>, reset, "
+                    "pack, merge)";
+    if (buf && len > 0) {
+        strncpy(buf, v, (size_t)len - 1);
+        buf[len - 1] = 0;
+    }
+    return 8;
+}
+
+int smx_nparts_for(int32_t rows, int32_t m) { return nparts_for(rows, m); }
+
+int smx_reset(const double* T, const smx_shape* shape, int32_t parity, int32_t clear_count,
+              smx_ctl* ctl, void* stream) {
+    if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_reset, dim3(1), dim3(1024), 0, S(stream), T, shape->ld, shape->rows,
+                       shape->m, fscan_of(*shape), shape->row0, parity & 1, clear_count, ctl);
+    return (int)hipGetLastError();
+}
+
+int smx_select(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+               smx_part* parts, void* stream) {
+    if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
+    return launch_select(T, *shape, parity & 1, ctl, parts, S(stream));
+}
+
+int smx_finalize(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                 const smx_part* parts, void* stream) {
+    if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kWave), 0, S(stream), parts, shape->nparts,
+                       parity & 1, shape->n, shape->m, shape->flen, T, shape->ld, ctl);
+    return (int)hipGetLastError();
+}
+
+int smx_update(const double* Tin, double* Tout, const smx_shape* shape, int32_t parity,
+               smx_ctl* ctl, const smx_part* parts, int32_t* log, int64_t log_cap,
+               void* stream) {
+    if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
+    return launch_update(Tin, Tout, *shape, parity & 1, ctl, parts, log, log_cap, S(stream));
+}
+
+int smx_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+            smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream) {
+    if (!shape_ok(shape) || buf0 == buf1 || k < 0) return (int)hipErrorInvalidValue;
+    return launch_chain(buf0, buf1, *shape, parity & 1, k, ctl, parts, log, log_cap, S(stream));
+}
+
+int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                  smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream,
+                  float* host_update_ms, float* host_total_ms) {
+    if (!shape_ok(shape) || buf0 == buf1 || k < 1 || !host_update_ms || !host_total_ms)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    const int p0 = parity & 1;
+    hipEvent_t* ev = new hipEvent_t[2 * (size_t)k + 1];
+    int err = 0;
+    for (int i = 0; i < 2 * k + 1; ++i) {
+        if (hipEventCreate(&ev[i]) != hipSuccess) {
+            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+            delete[] ev;
+            return (int)hipErrorOutOfMemory;
+        }
+    }
+    (void)hipEventRecord(ev[2 * k], st);
+    for (int step = 0; step < k && !err; ++step) {
+        const int p = (p0 + step) & 1;
+        double* tin = p ? buf1 : buf0;
+        double* tout = p ? buf0 : buf1;
+        err = launch_select(tin, *shape, p, ctl, parts, st);
+        if (err) break;
+        (void)hipEventRecord(ev[2 * step], st);
+        err = launch_update(tin, tout, *shape, p, ctl, parts, log, log_cap, st);
+        (void)hipEventRecord(ev[2 * step + 1], st);
+    }
+    if (!err) err = (int)hipEventSynchronize(ev[2 * k - 1]);
+    if (!err) {
+        for (int step = 0; step < k; ++step)
+            (void)hipEventElapsedTime(&host_update_ms[step], ev[2 * step], ev[2 * step + 1]);
+        (void)hipEventElapsedTime(host_total_ms, ev[2 * k], ev[2 * k - 1]);
+    }
+    for (int i = 0; i < 2 * k + 1; ++i) (void)hipEventDestroy(ev[i]);
+    delete[] ev;
+    return err;
+}
+
+int smx_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                     int32_t k, smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap,
+                     void* stream, void** graph_out) {
+    if (!shape_ok(shape) || buf0 == buf1 || k < 1 || !graph_out) return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    Graph* g = new Graph();
+    hipError_t err = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+    if (err != hipSuccess) {
+        delete g;
+        return (int)err;
+    }
+    int lerr = launch_chain(buf0, buf1, *shape, parity & 1, k, ctl, parts, log, log_cap, st);
+    err = hipStreamEndCapture(st, &g->graph);
+    if (lerr || err != hipSuccess) {
+        if (g->graph) (void)hipGraphDestroy(g->graph);
+        delete g;
+        return lerr ? lerr : (int)err;
+    }
+    err = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+    if (err != hipSuccess) {
+        (void)hipGraphDestroy(g->graph);
+        delete g;
+        return (int)err;
+    }
+    *graph_out = g;
+    return 0;
+}
+
+int smx_graph_launch(void* graph, void* stream) {
+    if (!graph) return (int)hipErrorInvalidValue;
+    return (int)hipGraphLaunch(static_cast<Graph*>(graph)->exec, S(stream));
+}
+
+int smx_graph_destroy(void* graph) {
+    if (!graph) return 0;
+    Graph* g = static_cast<Graph*>(graph);
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    if (g->graph) (void)hipGraphDestroy(g->graph);
+    delete g;
+    return 0;
+}
+
+int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, int32_t r,
+                      int32_t c, void* stream) {
+    if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
+    if (r < 0 || r >= shape->rows || c < 0 || c > shape->m) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_update<kForced>, dim3(update_grid(*shape)), dim3(kUpdBlock), 0,
+                       S(stream), Tin, Tout, shape->ld, shape->rows, shape->n, shape->m,
+                       shape->flen, fscan_of(*shape), shape->row0, 0, (smx_ctl*)nullptr,
+                       (const smx_part*)nullptr, 0, (int32_t*)nullptr, (int64_t)0,
+                       (const double*)nullptr, r, c);
+    return (int)hipGetLastError();
+}
+
+int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
+                   const smx_part* parts, double* send, void* stream) {
+    if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
+    int blocks = (int)((shape->m + 2 + kUpdBlock - 1) / kUpdBlock);
+    if (blocks > 64) blocks = 64;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(kUpdBlock), 0, S(stream), T, shape->ld,
+                       shape->rows, shape->m, shape->row0, parity & 1, ctl, parts,
+                       shape->nparts, send);
+    return (int)hipGetLastError();
+}
+
+int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,
+                    int32_t parity, smx_ctl* ctl, int32_t* log, int64_t log_cap, void* stream) {
+    (void)parity;
+    if (!shape_ok(shape) || nranks < 1) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_merge, dim3(1), dim3(1024), 0, S(stream), recv, nranks, shape->ld,
+                       shape->n, shape->m, shape->flen, ctl, log, log_cap);
+    return (int)hipGetLastError();
+}
+
+int smx_shard_update(const double* Tin, double* Tout, const double* recv,
+                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, void* stream) {
+    if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_update<kShard>, dim3(update_grid(*shape)), dim3(kUpdBlock), 0,
+                       S(stream), Tin, Tout, shape->ld, shape->rows, shape->n, shape->m,
+                       shape->flen, fscan_of(*shape), shape->row0, parity & 1, ctl,
+                       (const smx_part*)nullptr, 0, (int32_t*)nullptr, (int64_t)0, recv, 0, 0);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

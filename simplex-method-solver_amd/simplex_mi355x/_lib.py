@@ -1,0 +1,99 @@
+"""ctypes binding of ``libsmx.so`` (the C ABI declared in ``include/smx.h``).
+
+The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()`` runs it).  There
+is no fallback of any kind: if the library is missing or fails to load, importing the engine
+raises, so nothing can silently run on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsmx.so")
+
+# outcome codes, include/smx.h
+PIVOT, OPTIMUM, INCORRECT, NOT_CONVERGE, FSHORT, IDLE = 0, 1, 2, 3, 4, 5
+NONE = 0x7F7F7F7F
+SHARD_HDR = 8
+CTL_BYTES = 128
+PART_BYTES = 32
+
+# numpy view of struct smx_ctl (include/smx.h)
+CTL_DTYPE = np.dtype([
+    ("negb", "<i4", (2,)), ("negf", "<i4", (2,)), ("term", "<i4"), ("sel_status", "<i4"),
+    ("sel_r", "<i4"), ("sel_c", "<i4"), ("sel_e", "<f8"), ("npivots", "<i8"),
+    ("sel_owner", "<i4"), ("pad0", "<i4"), ("reserved", "<i8", (9,)),
+])
+assert CTL_DTYPE.itemsize == CTL_BYTES
+
+
+class Shape(ctypes.Structure):
+    """struct smx_shape (include/smx.h)."""
+    _fields_ = [("ld", ctypes.c_int64), ("rows", ctypes.c_int32), ("n", ctypes.c_int32),
+                ("m", ctypes.c_int32), ("flen", ctypes.c_int32), ("row0", ctypes.c_int32),
+                ("nparts", ctypes.c_int32)]
+
+
+_lib = None
+
+EXPORTS = (
+    "smx_version", "smx_nparts_for", "smx_reset", "smx_select", "smx_finalize", "smx_update",
+    "smx_run", "smx_run_timed", "smx_graph_create", "smx_graph_launch", "smx_graph_destroy", "smx_update_forced",
+    "smx_shard_pack", "smx_shard_merge", "smx_shard_update",
+)
+
+
+def load():
+    """Load libsmx.so once; raises OSError if it is missing (build it with csrc/Makefile)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # torch first: libsmx.so and torch's bundled runtime share the SONAME libamdhip64.so.7, and
+    # the engine must run on the runtime torch already initialised (one HIP runtime per process)
+    import torch  # noqa: F401
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} not built: run `make -C simplex-method-solver_amd/csrc` "
+                      "(or __graft_entry__.build()); the engine has no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sp = ctypes.POINTER(Shape)
+    sig = {
+        "smx_version": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+        "smx_nparts_for": ([i32, i32], ctypes.c_int),
+        "smx_reset": ([vp, sp, i32, i32, vp, vp], ctypes.c_int),
+        "smx_select": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),
+        "smx_finalize": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),
+        "smx_update": ([vp, vp, sp, i32, vp, vp, vp, i64, vp], ctypes.c_int),
+        "smx_run": ([vp, vp, sp, i32, i32, vp, vp, vp, i64, vp], ctypes.c_int),
+        "smx_run_timed": ([vp, vp, sp, i32, i32, vp, vp, vp, i64, vp,
+                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)],
+                          ctypes.c_int),
+        "smx_graph_create": ([vp, vp, sp, i32, i32, vp, vp, vp, i64, vp,
+                              ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "smx_graph_launch": ([vp, vp], ctypes.c_int),
+        "smx_graph_destroy": ([vp], ctypes.c_int),
+        "smx_update_forced": ([vp, vp, sp, i32, i32, vp], ctypes.c_int),
+        "smx_shard_pack": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
+        "smx_shard_merge": ([vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
+        "smx_shard_update": ([vp, vp, vp, sp, i32, vp, vp], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def version() -> str:
+    buf = ctypes.create_string_buffer(256)
+    load().smx_version(buf, 256)
+    return buf.value.decode()
+
+
+def check(err: int, what: str) -> None:
+    if err != 0:
+        raise RuntimeError(f"{what} failed with hipError {err}")

@@ -1,0 +1,237 @@
+"""Device-resident tableau: HBM layout, control block and the pivot launches.
+
+Layout in HBM (one object per tableau, owned by torch tensors):
+
+* ``buf``   : ``float64[2][R][ld]`` ping-pong tableaux; step ``s`` reads ``buf[s & 1]`` and writes
+  ``buf[(s+1) & 1]`` (the reference is out of place as well: deepcopy at simplex.py:149/177).
+  ``R = rows + 1`` (constraint rows, then the f-row), ``C = m + 1`` used columns, ``ld`` = C
+  rounded up to an even count and to 16 doubles (128-B rows, 16-B ``double2`` lanes).
+* ``ctl``   : 128-B ``struct smx_ctl`` (first-negative slots, selection, pivot counter).
+* ``parts`` : ``nparts`` x 32-B ``struct smx_part`` select partials.
+* ``log``   : ``int32[log_cap][2]`` ring of applied pivots ``(r, c)``, drained by the host.
+
+All launches go to one dedicated HIP stream per tableau; the host synchronises only when it
+reads the control block.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+
+
+def leading_dim(C: int, pad_to: int = 16) -> int:
+    ce = C + (C & 1)
+    return ((ce + pad_to - 1) // pad_to) * pad_to
+
+
+class Graph:
+    """A captured chain of k pivots (hipGraph); replayed by :meth:`launch`."""
+
+    def __init__(self, handle: int):
+        self.handle = handle
+
+    def launch(self, stream: int) -> None:
+        _lib.check(_lib.load().smx_graph_launch(self.handle, stream), "smx_graph_launch")
+
+    def destroy(self) -> None:
+        if self.handle:
+            _lib.load().smx_graph_destroy(self.handle)
+            self.handle = None
+
+
+class DeviceTableau:
+    """A dense fp64 tableau in HBM plus the state of the pivot loop."""
+
+    def __init__(self, dense: np.ndarray, n: int, m: int, flen: int, *, device=None,
+                 row0: int = 0, n_global: int | None = None, log_cap: int = 1 << 16,
+                 pad_to: int = 16):
+        if not torch.cuda.is_available():
+            raise RuntimeError("simplex_mi355x needs an MI355X (HIP device); there is no CPU path")
+        _lib.load()
+        rows = dense.shape[0] - 1
+        C = m + 1
+        if dense.shape[1] < C:
+            raise ValueError("dense tableau narrower than m + 1")
+        self.device = torch.device(device if device is not None else "cuda")
+        self.rows, self.n, self.m, self.flen, self.row0 = rows, (n if n_global is None else n_global), m, flen, row0
+        self.C = C
+        self.ld = leading_dim(C, pad_to)
+        self.nparts = _lib.load().smx_nparts_for(rows, m)
+        self.shape = [self.ld, rows, self.n, m, flen, row0, self.nparts]
+        self.stream = torch.cuda.Stream(self.device)
+        with torch.cuda.stream(self.stream):
+            self.buf = torch.zeros((2, rows + 1, self.ld), dtype=torch.float64, device=self.device)
+            self.ctl = torch.zeros(_lib.CTL_BYTES // 8, dtype=torch.int64, device=self.device)
+            self.parts = torch.zeros(self.nparts * _lib.PART_BYTES // 8, dtype=torch.int64,
+                                     device=self.device)
+            self.log = torch.zeros(2 * log_cap, dtype=torch.int32, device=self.device)
+        self.log_cap = log_cap
+        self.step = 0
+        self._pending = False   # chained pivots enqueued whose outcome the host has not read
+        self._term = False      # a terminal outcome may be latched in ctl.term
+        self._graphs: dict[tuple[int, int], Graph] = {}
+        self.upload(dense)
+
+    # -- data movement --------------------------------------------------------------------
+    def upload(self, dense: np.ndarray) -> None:
+        """Copy a host tableau into buf[0] and prime the control block (pivot count = 0)."""
+        host = torch.from_numpy(np.ascontiguousarray(dense[:, :self.C], dtype=np.float64))
+        with torch.cuda.stream(self.stream):
+            self.buf.zero_()
+            self.buf[0, :, :self.C].copy_(host)
+            self.step = 0
+            ops.reset(self.buf[0], self.ctl, self.shape, 0, 1)
+        self._pending = False
+        self._term = False
+
+    def settle(self) -> None:
+        """Make the host step counter exact after chained pivots (one control-block read)."""
+        if self._pending:
+            self.sync_state()
+
+    def cur(self) -> torch.Tensor:
+        self.settle()
+        return self.buf[self.step & 1]
+
+    def download(self) -> np.ndarray:
+        with torch.cuda.stream(self.stream):
+            out = self.cur()[:, :self.C].cpu().numpy()
+        return out
+
+    def values(self, idx) -> list[float]:
+        """Host copies of selected elements [(i, j), ...] of the current tableau."""
+        if not idx:
+            return []
+        ii = torch.tensor([i for i, _ in idx], device=self.device)
+        jj = torch.tensor([j for _, j in idx], device=self.device)
+        with torch.cuda.stream(self.stream):
+            return self.cur()[ii, jj].cpu().tolist()
+
+    def read_ctl(self) -> np.void:
+        with torch.cuda.stream(self.stream):
+            raw = self.ctl.cpu().numpy()
+        return raw.view(_lib.CTL_DTYPE)[0]
+
+    def read_log(self, start: int, stop: int) -> np.ndarray:
+        """Pivots start..stop-1 (absolute counts) from the device ring."""
+        if stop <= start:
+            return np.zeros((0, 2), dtype=np.int32)
+        if stop - start > self.log_cap:
+            raise RuntimeError("pivot log overrun: drain the log more often")
+        with torch.cuda.stream(self.stream):
+            ring = self.log.cpu().numpy().reshape(-1, 2)
+        pos = np.arange(start, stop) % self.log_cap
+        return ring[pos]
+
+    # -- pivot loop -----------------------------------------------------------------------
+    def select(self) -> None:
+        with torch.cuda.stream(self.stream):
+            ops.select(self.cur(), self.ctl, self.parts, self.shape, self.step & 1)
+
+    def pick(self):
+        """pick_element on the device: returns (status, r, c, e); synchronises."""
+        self.settle()
+        if self._term:
+            self.clear_term()
+        with torch.cuda.stream(self.stream):
+            p = self.step & 1
+            ops.select(self.cur(), self.ctl, self.parts, self.shape, p)
+            ops.finalize(self.cur(), self.ctl, self.parts, self.shape, p)
+        c = self.read_ctl()
+        return int(c["sel_status"]), int(c["sel_r"]), int(c["sel_c"]), float(c["sel_e"])
+
+    def apply_selected(self) -> None:
+        """recalculate_matrix with the selection of the last select() (no host sync)."""
+        self.settle()
+        p = self.step & 1
+        with torch.cuda.stream(self.stream):
+            ops.update(self.buf[p], self.buf[p ^ 1], self.ctl, self.parts, self.log, self.shape, p)
+        self.step += 1
+
+    def run(self, k: int, graph: bool = True) -> None:
+        """Enqueue k chained pivots (no host sync).  Call :meth:`sync_state` afterwards."""
+        if k <= 0:
+            return
+        self.settle()
+        if self._term:
+            self.clear_term()
+        p = self.step & 1
+        with torch.cuda.stream(self.stream):
+            if graph:
+                g = self._graphs.get((p, k))
+                if g is None:
+                    g = self._make_graph(p, k)
+                g.launch(self.stream.cuda_stream)
+            else:
+                ops.run(self.buf, self.ctl, self.parts, self.log, self.shape, p, k)
+        # optimistic: if the chain stops early every later kernel is a no-op, and sync_state()
+        # replaces this with the device's exact count
+        self.step += k
+        self._pending = True
+
+    def run_timed(self, k: int):
+        """k chained pivots with HIP events around every update kernel (synchronous).
+        Returns (per-update-kernel ms array, device ms of the whole chain)."""
+        import ctypes
+        self.settle()
+        if self._term:
+            self.clear_term()
+        p = self.step & 1
+        upd = (ctypes.c_float * k)()
+        tot = ctypes.c_float()
+        sh = ops.make_shape(self.shape)
+        _lib.check(_lib.load().smx_run_timed(
+            self.buf[0].data_ptr(), self.buf[1].data_ptr(), ctypes.byref(sh), p, k,
+            self.ctl.data_ptr(), self.parts.data_ptr(), self.log.data_ptr(), self.log_cap,
+            self.stream.cuda_stream, upd, ctypes.byref(tot)), "smx_run_timed")
+        self.step += k
+        self._pending = True
+        return np.frombuffer(upd, dtype=np.float32).copy(), float(tot.value)
+
+    def sync_state(self) -> np.void:
+        """Read the control block and set the host step counter to the device pivot count."""
+        c = self.read_ctl()
+        self.step = int(c["npivots"])
+        self._pending = False
+        self._term = bool(c["term"])
+        return c
+
+    def clear_term(self) -> None:
+        """Re-arm the chain after a terminal outcome (the table is unchanged by it)."""
+        with torch.cuda.stream(self.stream):
+            self.ctl.view(torch.int32)[4] = 0   # smx_ctl.term (byte offset 16)
+        self._term = False
+
+    def _make_graph(self, parity: int, k: int) -> Graph:
+        import ctypes
+        h = ctypes.c_void_p()
+        sh = ops.make_shape(self.shape)
+        b0, b1 = self.buf[0].data_ptr(), self.buf[1].data_ptr()
+        _lib.check(_lib.load().smx_graph_create(
+            b0, b1, ctypes.byref(sh), parity, k, self.ctl.data_ptr(), self.parts.data_ptr(),
+            self.log.data_ptr(), self.log_cap, self.stream.cuda_stream, ctypes.byref(h)),
+            "smx_graph_create")
+        g = Graph(h.value)
+        self._graphs[(parity, k)] = g
+        return g
+
+    def forced(self, r: int, c: int) -> None:
+        """Forced pivot (no selection, no bookkeeping): buf[s&1] -> buf[(s+1)&1]."""
+        self.settle()
+        p = self.step & 1
+        with torch.cuda.stream(self.stream):
+            ops.update_forced(self.buf[p], self.buf[p ^ 1], self.shape, r, c)
+        self.step += 1
+
+    def close(self) -> None:
+        for g in self._graphs.values():
+            g.destroy()
+        self._graphs.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,294 @@
+"""``SimplexMethod`` / ``Info`` / ``Error`` -- the reference's solver surface, backed by HBM.
+
+Mirrors ``/root/reference/src/simplex.py`` (jqnfxa/Simplex-Method-Solver @ 2025-06-20):
+same constructor, attributes, method names, return tuples, snapshot objects and error
+strings, so ``main.py:13`` (``from simplex import SimplexMethod, Error``) and
+``table_widget.py:7`` (``from simplex import Info``) work unchanged through the ``simplex.py``
+drop-in next to this package.  The tableau lives on the MI355X; every selection and every
+pivot is a HIP kernel (``ops.py`` -> ``libsmx.so``).  There is no CPU fallback: without a
+device, construction raises.
+
+Additions (not in the reference, all opt-in): ``step()`` (one pick + pivot), ``solve()``
+(``get_solution`` with an optional pivot cap, or the chained no-history fast path),
+``pivots`` / ``pivot_log`` and ``status``.
+
+Deliberate differences, all on inputs the reference UI never produces (main.py:309-312 always
+passes rectangular float rows and ``len(function) == m``):
+* ragged constraint rows raise ``ValueError`` (the device tableau is dense);
+* integer inputs are held as fp64 on the device; integer arithmetic in the reference can differ
+  only in the sign of a zero on the first pivot, which no comparison in the rules can see.
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+
+from . import _lib
+from .device import DeviceTableau
+
+MESSAGES = {_lib.INCORRECT: "incorrect system",                  # simplex.py:89
+            _lib.NOT_CONVERGE: "simplex method does not converge"}  # simplex.py:139
+
+
+class Error:
+    """simplex.py:4-9."""
+
+    def __init__(self, error_string):
+        self.error_string = error_string
+
+    def __str__(self):
+        return self.error_string
+
+
+class Info:
+    """simplex.py:12-21: one step snapshot (labels and table copied)."""
+
+    def __init__(self, row, column, table, i, j, x1, x2, optimum):
+        self.row = row.copy()
+        self.column = column.copy()
+        self.table = copy.deepcopy(table)
+        self.i = i
+        self.j = j
+        self.x1 = x1
+        self.x2 = x2
+        self.optimum = optimum
+
+
+def _dense_from_lists(constraints, function, m):
+    n = len(constraints)
+    T = np.zeros((n + 1, m + 1), dtype=np.float64)
+    if n:
+        T[:n, :] = np.asarray(constraints, dtype=np.float64)
+    k = min(len(function), m + 1)
+    if k:
+        T[n, :k] = np.asarray(function[:k], dtype=np.float64)
+    return T
+
+
+class SimplexMethod:
+    """simplex.py:24-199 on an MI355X-resident tableau."""
+
+    def __init__(self, constraints, function, device=None):
+        # simplex.py:26-33 (IndexError on an empty constraint list, like the reference)
+        self.n = len(constraints)
+        self.m = len(constraints[0]) - 1
+        self.invalid_index = 1 + max(self.n, self.m)
+        self.function = function
+        self.row = ['x' + str(_) for _ in range(1, self.m + 1)]
+        self.column = ['y' + str(_) for _ in range(1, self.n + 1)]
+        self.row.append('-b')
+        self.column.append('f')
+        if any(len(c) != self.m + 1 for c in constraints):
+            raise ValueError("ragged constraint rows: the device tableau is dense "
+                             f"(every row must have m + 1 = {self.m + 1} entries)")
+        # simplex.py:36-39: the caller's rows (and function) by reference, until the first pivot
+        self._initial = [constraint for constraint in constraints]
+        self._initial.append(function)
+        self.flen = len(function)
+        self._dev = DeviceTableau(_dense_from_lists(constraints, function, self.m),
+                                  self.n, self.m, self.flen, device=device)
+        self._pristine = True
+        self.pivot_log: list[tuple[int, int]] = []
+        self.status = "ready"
+
+    # ---------------------------------------------------------------- state views --------
+    @property
+    def table(self):
+        """The current tableau as the reference's list of lists (f-row has len(function))."""
+        if self._pristine:
+            return self._initial
+        T = self._dev.download()
+        rows = T[:self.n].tolist()
+        rows.append(T[self.n, :min(self.flen, self.m + 1)].tolist())
+        return rows
+
+    @table.setter
+    def table(self, value):
+        cons, func = value[:-1], value[-1]
+        if any(len(c) != self.m + 1 for c in cons) or len(cons) != self.n:
+            raise ValueError("table shape does not match this problem")
+        self._initial = list(value)
+        self.flen = len(func)
+        self._dev.upload(_dense_from_lists(cons, func, self.m))
+        self._pristine = True
+
+    @property
+    def pivots(self) -> int:
+        return len(self.pivot_log)
+
+    def print_table(self):
+        """simplex.py:41-46."""
+        table = self.table
+        print("\t", end='')
+        print("\t".join(self.row))
+        for row in range(self.n + 1):
+            print(self.column[row], end='\t')
+            print("\t".join([str(round(val, 6)) for val in table[row]]))
+
+    def f(self, x1, x2):
+        """simplex.py:48-49 (on the ORIGINAL objective list)."""
+        return self.function[0] * x1 + self.function[1] * x2
+
+    def _last_of_rows(self, rows):
+        if self._pristine:
+            return [self._initial[i][-1] for i in rows]
+        last = [(i, self.m if i < self.n else min(self.flen, self.m + 1) - 1) for i in rows]
+        return self._dev.values(last)
+
+    def find_optimum(self) -> (float, float):
+        """simplex.py:51-68."""
+        def index_of(s):
+            for row in range(len(self.column)):
+                if self.column[row] == s:
+                    return row
+            return self.invalid_index
+
+        x1_i = index_of('x1')
+        x2_i = index_of('x2')
+        want = [i for i in (x1_i, x2_i) if i != self.invalid_index]
+        vals = dict(zip(want, self._last_of_rows(want)))
+        x1 = vals[x1_i] if x1_i != self.invalid_index else 0
+        x2 = vals[x2_i] if x2_i != self.invalid_index else 0
+        return x1, x2
+
+    # ---------------------------------------------------------------- the hot path -------
+    def pick_element(self) -> (bool, int, int, float):
+        """simplex.py:70-141: selection kernels on the device, outcome mapped to the
+        reference's return tuple / ValueError."""
+        status, r, c, e = self._dev.pick()
+        if status == _lib.PIVOT:
+            if self._pristine:
+                e = self._initial[r][c]
+            return True, r, c, e
+        if status == _lib.OPTIMUM:
+            x1, x2 = self.find_optimum()
+            return False, x1, x2, self.f(x1, x2)
+        if status in MESSAGES:
+            raise ValueError(MESSAGES[status])
+        if status == _lib.FSHORT:
+            # the reference indexes function[idx] past its end (simplex.py:95-96)
+            raise IndexError("list index out of range")
+        raise RuntimeError(f"unexpected selection status {status}")
+
+    def _apply(self, r, c):
+        """The part of recalculate_matrix after its pick_element (simplex.py:149-177)."""
+        self.row[c], self.column[r] = self.column[r], self.row[c]   # simplex.py:152
+        if self.flen > self.m + 1 or (self.flen < self.m and c >= self.flen):
+            # the reference's step 2 / step 4 index the f-row out of range (simplex.py:159-175)
+            raise IndexError("list index out of range")
+        self._dev.apply_selected()
+        self._pristine = False
+        self.pivot_log.append((r, c))
+
+    def recalculate_matrix(self):
+        """simplex.py:143-177."""
+        _is_successful, r, c, _ = self.pick_element()
+        if not _is_successful:
+            return
+        self._apply(r, c)
+
+    def get_solution(self, max_pivots=None):
+        """simplex.py:179-199.  ``max_pivots`` (default: none, as in the reference) bounds
+        cycling inputs; when it is hit the list simply ends and ``status == 'cap'``."""
+        result = []
+        result.append(Info(self.row, self.column, self.table, None, None, 0, 0, 0))
+        done = 0
+        while True:
+            try:
+                is_successful, i, j, e = self.pick_element()
+            except ValueError as exc:
+                result.append(Error(str(exc)))
+                self.status = "error"
+                return result
+            if not is_successful:
+                self.status = "optimum"
+                break
+            if max_pivots is not None and done >= max_pivots:
+                self.status = "cap"
+                break
+            result[-1].i = i
+            result[-1].j = j
+            self._apply(i, j)   # recalculate_matrix() without re-running the selection
+            done += 1
+            x1, x2 = self.find_optimum()
+            result.append(Info(self.row, self.column, self.table, None, None, x1, x2,
+                               self.f(x1, x2)))
+        return result
+
+    # ---------------------------------------------------------------- additions ----------
+    def step(self):
+        """One pick + pivot; returns pick_element's tuple (raises like it)."""
+        res = self.pick_element()
+        if res[0]:
+            self._apply(res[1], res[2])
+        return res
+
+    def solve(self, record_history=True, max_pivots=None, chunk=256, graph=True):
+        """``get_solution`` (record_history=True) or the chained fast path: pivots run on the
+        device in chunks of ``chunk`` with no host synchronisation inside a chunk; returns
+        ``[Info(initial, i/j of the first pivot), Info(final)]`` plus a trailing ``Error``."""
+        if record_history:
+            return self.get_solution(max_pivots=max_pivots)
+        if self.flen not in (self.m, self.m + 1) or self.flen < 2:
+            return self._solve_stepwise(max_pivots)
+        first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
+        start = self.pivots
+        budget = float("inf") if max_pivots is None else int(max_pivots)
+        dev = self._dev
+        status = None
+        while self.pivots - start < budget:
+            k = int(min(chunk, budget - (self.pivots - start), dev.log_cap))
+            before = dev.step
+            dev.run(k, graph=graph and k == chunk)
+            ctl = dev.sync_state()
+            done = int(ctl["npivots"])
+            for r, c in dev.read_log(before, done):
+                r, c = int(r), int(c)
+                self.row[c], self.column[r] = self.column[r], self.row[c]
+                self.pivot_log.append((r, c))
+            if done > 0:
+                self._pristine = False
+            if ctl["term"]:
+                status = int(ctl["sel_status"])
+                break
+        out = [first]
+        if self.pivots > start:
+            first.i, first.j = self.pivot_log[start]
+        x1, x2 = self.find_optimum()
+        out.append(Info(self.row, self.column, self.table, None, None, x1, x2, self.f(x1, x2)))
+        if status is None:
+            self.status = "cap"
+        elif status == _lib.OPTIMUM:
+            self.status = "optimum"
+        elif status in MESSAGES:
+            self.status = "error"
+            out.append(Error(MESSAGES[status]))
+        else:
+            raise RuntimeError(f"unexpected terminal status {status}")
+        return out
+
+    def _solve_stepwise(self, max_pivots):
+        first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
+        out = [first]
+        done = 0
+        while max_pivots is None or done < max_pivots:
+            try:
+                ok, i, j, _ = self.pick_element()
+            except ValueError as exc:
+                x1, x2 = self.find_optimum()
+                out.append(Info(self.row, self.column, self.table, None, None, x1, x2,
+                                self.f(x1, x2)))
+                out.append(Error(str(exc)))
+                self.status = "error"
+                return out
+            if not ok:
+                break
+            if done == 0:
+                first.i, first.j = i, j
+            self._apply(i, j)
+            done += 1
+        self.status = "optimum" if (max_pivots is None or done < max_pivots) else "cap"
+        x1, x2 = self.find_optimum()
+        out.append(Info(self.row, self.column, self.table, None, None, x1, x2, self.f(x1, x2)))
+        return out

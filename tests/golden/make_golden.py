@@ -47,10 +47,17 @@ def enc(v):
     raise TypeError(type(v))
 
 
+CANON_NAN = float("nan")
+
+
 def table_hash(table) -> str:
+    """SHA-256 of the table's fp64 bytes, every NaN canonicalised (NaN payload and sign are not
+    part of the contract: x86 and gfx950 propagate them differently)."""
     h = hashlib.sha256()
     for row in table:
-        h.update(struct.pack("<%dd" % len(row), *[float(x) for x in row]))
+        vals = [float(x) for x in row]
+        vals = [v if v == v else CANON_NAN for v in vals]
+        h.update(struct.pack("<%dd" % len(vals), *vals))
     return h.hexdigest()
 
 

@@ -32,17 +32,30 @@ def dec_input(inp):
     return dec_table(inp["constraints"]), [dec(x) for x in inp["function"]]
 
 
+CANON_NAN = float("nan")
+
+
 def table_hash(table) -> str:
+    """SHA-256 of the fp64 bytes, NaNs canonicalised (same rule as make_golden.table_hash)."""
     h = hashlib.sha256()
     for row in table:
-        h.update(struct.pack("<%dd" % len(row), *[float(x) for x in row]))
+        vals = [float(x) for x in row]
+        vals = [v if v == v else CANON_NAN for v in vals]
+        h.update(struct.pack("<%dd" % len(vals), *vals))
     return h.hexdigest()
+
+
+def canon(T: np.ndarray) -> np.ndarray:
+    """Copy with every NaN replaced by the canonical quiet NaN 0x7ff8000000000000."""
+    T = np.array(T, dtype="<f8", copy=True)
+    T[np.isnan(T)] = np.nan
+    return T
 
 
 def dense_hash(T: np.ndarray, n: int, flen: int) -> str:
     """Hash of a dense tableau in the reference's ragged layout (f-row trimmed to flen)."""
     h = hashlib.sha256()
-    T = np.ascontiguousarray(T, dtype="<f8")
+    T = canon(T)
     h.update(T[:n].tobytes())
     h.update(T[n, :flen].tobytes())
     return h.hexdigest()
