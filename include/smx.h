@@ -21,8 +21,8 @@
  *   - All pointers are DEVICE pointers owned by the caller (torch tensors in the Python host),
  *     except where a name says host.  Every call is asynchronous on `stream` (a hipStream_t).
  *   - Tableau: row-major fp64, R = n+1 rows (n constraint rows, then the f-row), C = m+1 used
- *     columns (m variables, then the "-b" column), leading dimension `ld` (even, >= C+1 when C is
- *     odd).  f-row entries j >= flen are padding: computed, never read by a selection.
+ *     columns (m variables, then the "-b" column), leading dimension `ld` (a multiple of 4 doubles,
+ *     >= C rounded up to 4).  f-row entries j >= flen are padding: computed, never read by a selection.
  *   - Two tableau buffers ping-pong: step s reads buf[s & 1] and writes buf[(s + 1) & 1];
  *     `parity` = s & 1 selects the control-block slots of that step.
  *   - Return value: 0 on success, otherwise a hipError_t (no exceptions cross this ABI).
@@ -88,6 +88,13 @@ typedef struct smx_shape {
 int smx_version(char* buf, int len);
 /* Recommended number of select partials for a shape (host-only helper). */
 int smx_nparts_for(int32_t rows, int32_t m);
+
+/* Tuning of the update kernel (process-wide): variant index (16-B loads in flight per lane,
+ * non-temporal stores; see smx_tune_get) and resident blocks per CU (0 = occupancy API).
+ * A negative argument keeps the current value. */
+int smx_tune_set(int32_t variant, int32_t blocks_per_cu);
+int smx_tune_get(int32_t* variant, int32_t* blocks_per_cu, int32_t* nvariants,
+                 int32_t* units_in_flight, int32_t* vec, int32_t* nt);
 
 /* Scan a freshly uploaded tableau into ctl slot `parity`; clears term, sets sel_status = IDLE,
  * and zeroes npivots when clear_count != 0. */

@@ -33,8 +33,6 @@ constexpr int kWave = 64;
 constexpr int kSelBlock = 256;
 constexpr int kUpdBlock = 256;
 constexpr int kUpdWaves = kUpdBlock / kWave;
-constexpr int kRowsPerTile = 8;      // rows per wave work unit (8 x 16 B loads in flight/lane)
-constexpr int kMaxUpdGrid = 2048;    // 256 CUs x 8 resident blocks; grid-stride beyond
 constexpr int kMaxParts = 64;
 
 // ---------------------------------------------------------------------------------------------
@@ -313,16 +311,22 @@ __global__ __launch_bounds__(kWave) void k_finalize(const smx_part* __restrict__
 // ---------------------------------------------------------------------------------------------
 // k_update: the modified Jordan step (simplex.py:149-177), out of place.
 //
-// Work unit = one wave x kRowsPerTile rows x 64 lanes x 2 doubles (a 1 KiB column chunk per
-// row): per row one 16-B load + one 16-B store per lane, the pivot-row chunk held in registers
-// for all rows of the unit, T[i][c] a wave-uniform scalar load.  Per element:
+// Streaming shape (measured on MI355X with tools/hbm_probe.hip: a grid-wide sweep in address
+// order, where every resident wave works inside one narrow moving window of the tableau, streams
+// faster than per-wave private regions).  A unit is one row x one chunk of 64 lanes x 2 doubles
+// (1 KiB); unit u = row * nchunks + chunk; wave w takes units w, w + NW, w + 2 NW, ... in
+// batches of U (U 16-B loads in flight per lane before any arithmetic).  When NW is a multiple
+// of nchunks a wave always sees the same chunk, so its pivot-row slice stays in registers.
+// T[i][c] is a wave-uniform scalar load per unit.  Per element:
 //     num = (i == r) ? (j == c ? 1.0 : -x)          steps 1 and 3
 //                    : (j == c ? x   : x*e - pr*pc) steps 2 and 4
 //     out = num / e
 // which is exactly the value the reference leaves in new_table[i][j] after steps 1-4.
 enum UpdMode { kSingle = 0, kShard = 1, kForced = 2 };
 
-template <int MODE>
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+template <int MODE, int U, bool NT>
 __global__ __launch_bounds__(kUpdBlock) void k_update(
     const double* __restrict__ Tin, double* __restrict__ Tout, int64_t ld, int rows_local,
     int n, int m, int flen, int fscan, int row0, int parity, smx_ctl* __restrict__ ctl,
@@ -381,67 +385,83 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     const int r_local = r - row0;  // may be outside [0, rows_local): pivot row lives elsewhere
     const int R = rows_local + 1;  // + the f-row (local row rows_local)
     const int C = m + 1;
-    const int vpr = (C + 1) >> 1;                     // 2-double vectors per row
-    const int nchunks = (vpr + kWave - 1) / kWave;    // 64-vector chunks per row
-    const int rtiles = (R + kRowsPerTile - 1) / kRowsPerTile;
-    const int64_t units = (int64_t)nchunks * rtiles;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int kChunk = kWave * 2;                  // doubles per unit
+    const int nchunks = (C + kChunk - 1) / kChunk;
+    const int64_t units = (int64_t)nchunks * R;
+    const int NW = gridDim.x * kUpdWaves;
+    const int w = blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(tid >> 6);
+    // unit u = i * nchunks + ch; advancing u by NW advances (i, ch) by (qs, rs)
+    const int qs = NW / nchunks, rs = NW % nchunks;
+    int i_cur = w / nchunks, ch_cur = w % nchunks;
+    int ch_pr = -1;
+    dbl2 pr = dbl2{0.0, 0.0};
     const int negslot = parity ^ 1;
     int lb = SMX_NONE;   // fused next-step scan: first row with new b < 0 (this lane)
     int lf = SMX_NONE;   // fused next-step scan: first f-row column with new f < 0 (this lane)
 
-    for (int64_t u = (int64_t)blockIdx.x * kUpdWaves + wid; u < units;
-         u += (int64_t)gridDim.x * kUpdWaves) {
-        const int ch = (int)(u % nchunks);
-        const int i0 = (int)(u / nchunks) * kRowsPerTile;
-        const int v = ch * kWave + lane;
-        const bool active = v < vpr;
-        const int j = 2 * v;
-        double2 pr = make_double2(0.0, 0.0);
-        if (active) pr = *reinterpret_cast<const double2*>(prow + j);
-        double2 x[kRowsPerTile];
-        double pc[kRowsPerTile];
+    for (int64_t u = w; u < units; u += (int64_t)U * NW) {
+        int iu[U], chu[U];
+        dbl2 x[U];
+        double pc[U];
 #pragma unroll
-        for (int k = 0; k < kRowsPerTile; ++k) {
-            const int i = i0 + k;
-            pc[k] = 0.0;
-            x[k] = make_double2(0.0, 0.0);
-            if (i < R) {
-                const double* src = Tin + (int64_t)i * ld;
-                pc[k] = src[c];
-                if (active) x[k] = *reinterpret_cast<const double2*>(src + j);
+        for (int k = 0; k < U; ++k) {
+            iu[k] = i_cur;
+            chu[k] = ch_cur;
+            ch_cur += rs;
+            i_cur += qs;
+            if (ch_cur >= nchunks) {
+                ch_cur -= nchunks;
+                ++i_cur;
             }
         }
 #pragma unroll
-        for (int k = 0; k < kRowsPerTile; ++k) {
-            const int i = i0 + k;
-            if (i >= R) break;
-            double n0, n1;
-            if (i == r_local) {
-                n0 = (j == c) ? 1.0 : -x[k].x;
-                n1 = (j + 1 == c) ? 1.0 : -x[k].y;
-            } else {
-                const double a0 = x[k].x * e;
-                const double b0 = pr.x * pc[k];
-                const double a1 = x[k].y * e;
-                const double b1 = pr.y * pc[k];
-                n0 = (j == c) ? x[k].x : (a0 - b0);
-                n1 = (j + 1 == c) ? x[k].y : (a1 - b1);
+        for (int k = 0; k < U; ++k) {
+            x[k] = dbl2{0.0, 0.0};
+            pc[k] = 0.0;
+            if (iu[k] < R) {
+                const double* src = Tin + (int64_t)iu[k] * ld;
+                const int j = chu[k] * kChunk + 2 * lane;
+                pc[k] = src[c];
+                if (j < C) x[k] = *reinterpret_cast<const dbl2*>(src + j);
             }
-            double2 o;
-            o.x = n0 / e;
-            o.y = n1 / e;
-            if (active) {
-                *reinterpret_cast<double2*>(Tout + (int64_t)i * ld + j) = o;
-                if (MODE != kForced) {
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int i = iu[k];
+            if (i >= R) continue;
+            const int j = chu[k] * kChunk + 2 * lane;
+            if (chu[k] != ch_pr) {
+                ch_pr = chu[k];
+                pr = (j < C) ? *reinterpret_cast<const dbl2*>(prow + j) : dbl2{0.0, 0.0};
+            }
+            dbl2 o;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int jj = j + h;
+                const double xv = x[k][h];
+                double num;
+                if (i == r_local) {
+                    num = (jj == c) ? 1.0 : -xv;
+                } else {
+                    const double a = xv * e;
+                    const double b = pr[h] * pc[k];
+                    num = (jj == c) ? xv : (a - b);
+                }
+                o[h] = num / e;
+                if (MODE != kForced && jj < C) {
                     if (i < rows_local) {
-                        const double nb = (j == m) ? o.x : o.y;
-                        if ((j == m || j + 1 == m) && nb < 0.0) lb = min(lb, row0 + i);
-                    } else {
-                        if (j < fscan && o.x < 0.0) lf = min(lf, j);
-                        if (j + 1 < fscan && o.y < 0.0) lf = min(lf, j + 1);
+                        if (jj == m && o[h] < 0.0) lb = min(lb, row0 + i);
+                    } else if (jj < fscan && o[h] < 0.0) {
+                        lf = min(lf, jj);
                     }
                 }
+            }
+            if (j < C) {
+                double* dst = Tout + (int64_t)i * ld + j;
+                if (NT)
+                    __builtin_nontemporal_store(o, reinterpret_cast<dbl2*>(dst));
+                else
+                    *reinterpret_cast<dbl2*>(dst) = o;
             }
         }
     }
@@ -642,17 +662,6 @@ inline int nparts_for(int rows, int m) {
     return p;
 }
 
-inline int update_grid(const smx_shape& s) {
-    const int R = s.rows + 1;
-    const int vpr = (s.m + 2) >> 1;
-    const int64_t nchunks = (vpr + kWave - 1) / kWave;
-    const int64_t units = nchunks * ((R + kRowsPerTile - 1) / kRowsPerTile);
-    int64_t blocks = (units + kUpdWaves - 1) / kUpdWaves;
-    if (blocks > kMaxUpdGrid) blocks = kMaxUpdGrid;
-    if (blocks < 1) blocks = 1;
-    return (int)blocks;
-}
-
 inline int fscan_of(const smx_shape& s) { return s.flen < s.m ? s.flen : s.m; }
 
 inline bool shape_ok(const smx_shape* s) {
@@ -660,6 +669,7 @@ inline bool shape_ok(const smx_shape* s) {
     if (s->m < 0 || s->rows < 0 || s->n < s->rows || s->ld < s->m + 1) return false;
     if ((s->ld & 1) != 0) return false;                   // 16-B aligned double2 rows
     if (((s->m + 1) & 1) && s->ld < s->m + 2) return false;  // odd C: vector tail in padding
+    if ((s->m + 1) > 2 && (s->ld & 3) != 0) return false;    // VEC = 4 variants: 32-B lanes
     if (s->nparts < 1 || s->nparts > kMaxParts) return false;
     return true;
 }
@@ -673,12 +683,117 @@ int launch_select(const double* T, const smx_shape& s, int parity, smx_ctl* ctl,
     return (int)hipGetLastError();
 }
 
+// ---- update-kernel variants (rows per unit TR, doubles per lane VEC, non-temporal stores) -----
+struct UpdVariant {
+    int u, nt;
+};
+constexpr UpdVariant kVariants[] = {{1, 0}, {2, 0}, {4, 0}, {8, 0}, {1, 1}, {2, 1}, {4, 1}, {8, 1}};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+// Defaults from tools/tune_update.py on MI355X at 16384^2 (profiles/r01_tune_sweep.jsonl):
+// U = 2 loads in flight per lane, non-temporal stores, 5 resident blocks (20 waves) per CU.
+int g_variant = 5;        // smx_tune_set overrides
+int g_blocks_per_cu = 0;  // 0: kDefaultBpc, capped by the occupancy API (see blocks_per_cu)
+constexpr int kDefaultBpc = 5;
+
+using UpdFn = void (*)(const double*, double*, int64_t, int, int, int, int, int, int, int,
+                       smx_ctl*, const smx_part*, int, int32_t*, int64_t, const double*, int, int);
+
+template <int MODE>
+UpdFn upd_fn(int v) {
+    switch (v) {
+        case 0: return k_update<MODE, 1, false>;
+        case 1: return k_update<MODE, 2, false>;
+        case 2: return k_update<MODE, 4, false>;
+        case 3: return k_update<MODE, 8, false>;
+        case 4: return k_update<MODE, 1, true>;
+        case 5: return k_update<MODE, 2, true>;
+        case 6: return k_update<MODE, 4, true>;
+        default: return k_update<MODE, 8, true>;
+    }
+}
+
+// Resident blocks per CU for a kernel, cached.  The grid is exactly CUs x this, so every block
+// is resident at once and the balanced unit ranges finish together (no second residency round).
+int blocks_per_cu(const void* fn) {
+    if (g_blocks_per_cu > 0) return g_blocks_per_cu;
+    struct Entry {
+        const void* fn;
+        int dev;
+        int bpc;
+    };
+    static Entry cache[128];
+    static int ncache = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    for (int i = 0; i < ncache; ++i)
+        if (cache[i].fn == fn && cache[i].dev == dev) return cache[i].bpc;
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kUpdBlock, 0) != hipSuccess ||
+        bpc < 1)
+        bpc = 4;
+    // ROCm 7.2 over-reports by one block/CU for 256-thread kernels above 80 SGPRs
+    // (MI355X_MICROARCH.md, residency): keep one block of margin below the API's answer.
+    if (bpc > 1) bpc -= 1;
+    if (bpc > kDefaultBpc) bpc = kDefaultBpc;
+    if (ncache < 128) cache[ncache++] = Entry{fn, dev, bpc};
+    return bpc;
+}
+
+int num_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) dev = 0;
+    if (!cus[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            v < 1)
+            v = 256;
+        cus[dev] = v;
+    }
+    return cus[dev];
+}
+
+// Grid = resident blocks, trimmed so the wave count is a multiple of the chunks per row (then
+// every wave keeps one pivot-row slice for the whole sweep).
+int update_grid(const smx_shape& s, int variant, const void* fn) {
+    (void)variant;
+    const int64_t R = s.rows + 1;
+    const int64_t nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
+    const int64_t units = nchunks * R;
+    int64_t blocks = (int64_t)num_cus() * blocks_per_cu(fn);
+    // waves = a multiple of lcm(nchunks, waves per block) when that keeps >= 3/4 of them
+    int64_t g = nchunks, h = kUpdWaves;
+    while (h) {
+        const int64_t t = g % h;
+        g = h;
+        h = t;
+    }
+    const int64_t lcm = nchunks / g * kUpdWaves;
+    const int64_t waves = blocks * kUpdWaves;
+    if (waves >= lcm && (waves - waves % lcm) * 4 >= waves * 3) blocks = (waves - waves % lcm) / kUpdWaves;
+    const int64_t need = (units + kUpdWaves - 1) / kUpdWaves;
+    if (blocks > need) blocks = need;
+    if (blocks < 1) blocks = 1;
+    return (int)blocks;
+}
+
+template <int MODE>
+int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int parity,
+                       smx_ctl* ctl, const smx_part* parts, int32_t* log, int64_t log_cap,
+                       const double* recv, int fr, int fc, hipStream_t st) {
+    const int v = g_variant;
+    UpdFn fn = upd_fn<MODE>(v);
+    hipLaunchKernelGGL(fn, dim3(update_grid(s, v, (const void*)fn)), dim3(kUpdBlock), 0, st, Tin,
+                       Tout, s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl,
+                       parts, s.nparts, log, log_cap, recv, fr, fc);
+    return (int)hipGetLastError();
+}
+
 int launch_update(const double* Tin, double* Tout, const smx_shape& s, int parity, smx_ctl* ctl,
                   const smx_part* parts, int32_t* log, int64_t log_cap, hipStream_t st) {
-    hipLaunchKernelGGL(k_update<kSingle>, dim3(update_grid(s)), dim3(kUpdBlock), 0, st, Tin, Tout,
-                       s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl, parts,
-                       s.nparts, log, log_cap, (const double*)nullptr, 0, 0);
-    return (int)hipGetLastError();
+    return launch_update_mode<kSingle>(Tin, Tout, s, parity, ctl, parts, log, log_cap, nullptr, 0,
+                                       0, st);
 }
 
 int launch_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, smx_ctl* ctl,
@@ -716,6 +831,24 @@ int smx_version(char* buf, int len) {
 }
 
 int smx_nparts_for(int32_t rows, int32_t m) { return nparts_for(rows, m); }
+
+int smx_tune_set(int32_t variant, int32_t blocks_per_cu_override) {
+    if (variant >= kNumVariants) return (int)hipErrorInvalidValue;
+    if (variant >= 0) g_variant = variant;
+    if (blocks_per_cu_override >= 0) g_blocks_per_cu = blocks_per_cu_override;
+    return 0;
+}
+
+int smx_tune_get(int32_t* variant, int32_t* blocks_per_cu_override, int32_t* nvariants,
+                 int32_t* units_in_flight, int32_t* vec, int32_t* nt) {
+    if (variant) *variant = g_variant;
+    if (blocks_per_cu_override) *blocks_per_cu_override = g_blocks_per_cu;
+    if (nvariants) *nvariants = kNumVariants;
+    if (units_in_flight) *units_in_flight = kVariants[g_variant].u;
+    if (vec) *vec = 2;
+    if (nt) *nt = kVariants[g_variant].nt;
+    return 0;
+}
 
 int smx_reset(const double* T, const smx_shape* shape, int32_t parity, int32_t clear_count,
               smx_ctl* ctl, void* stream) {
@@ -836,12 +969,8 @@ int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, i
                       int32_t c, void* stream) {
     if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
     if (r < 0 || r >= shape->rows || c < 0 || c > shape->m) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_update<kForced>, dim3(update_grid(*shape)), dim3(kUpdBlock), 0,
-                       S(stream), Tin, Tout, shape->ld, shape->rows, shape->n, shape->m,
-                       shape->flen, fscan_of(*shape), shape->row0, 0, (smx_ctl*)nullptr,
-                       (const smx_part*)nullptr, 0, (int32_t*)nullptr, (int64_t)0,
-                       (const double*)nullptr, r, c);
-    return (int)hipGetLastError();
+    return launch_update_mode<kForced>(Tin, Tout, *shape, 0, nullptr, nullptr, nullptr, 0,
+                                       nullptr, r, c, S(stream));
 }
 
 int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
@@ -868,11 +997,8 @@ int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,
 int smx_shard_update(const double* Tin, double* Tout, const double* recv,
                      const smx_shape* shape, int32_t parity, smx_ctl* ctl, void* stream) {
     if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_update<kShard>, dim3(update_grid(*shape)), dim3(kUpdBlock), 0,
-                       S(stream), Tin, Tout, shape->ld, shape->rows, shape->n, shape->m,
-                       shape->flen, fscan_of(*shape), shape->row0, parity & 1, ctl,
-                       (const smx_part*)nullptr, 0, (int32_t*)nullptr, (int64_t)0, recv, 0, 0);
-    return (int)hipGetLastError();
+    return launch_update_mode<kShard>(Tin, Tout, *shape, parity & 1, ctl, nullptr, nullptr, 0,
+                                      recv, 0, 0, S(stream));
 }
 
 }  // extern "C"

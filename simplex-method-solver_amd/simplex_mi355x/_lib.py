@@ -40,7 +40,7 @@ class Shape(ctypes.Structure):
 _lib = None
 
 EXPORTS = (
-    "smx_version", "smx_nparts_for", "smx_reset", "smx_select", "smx_finalize", "smx_update",
+    "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_reset", "smx_select", "smx_finalize", "smx_update",
     "smx_run", "smx_run_timed", "smx_graph_create", "smx_graph_launch", "smx_graph_destroy", "smx_update_forced",
     "smx_shard_pack", "smx_shard_merge", "smx_shard_update",
 )
@@ -63,6 +63,8 @@ def load():
     sig = {
         "smx_version": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
         "smx_nparts_for": ([i32, i32], ctypes.c_int),
+        "smx_tune_set": ([i32, i32], ctypes.c_int),
+        "smx_tune_get": ([ctypes.POINTER(i32)] * 6, ctypes.c_int),
         "smx_reset": ([vp, sp, i32, i32, vp, vp], ctypes.c_int),
         "smx_select": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),
         "smx_finalize": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),

@@ -22,8 +22,10 @@ from . import _lib, ops
 
 
 def leading_dim(C: int, pad_to: int = 16) -> int:
-    ce = C + (C & 1)
-    return ((ce + pad_to - 1) // pad_to) * pad_to
+    """Row stride in doubles: C rounded up to a multiple of ``pad_to`` (>= 4, so every 32-B
+    lane group of the VEC=4 update variants stays inside the row)."""
+    pad_to = max(4, pad_to - pad_to % 4)
+    return ((C + pad_to - 1) // pad_to) * pad_to
 
 
 class Graph:
@@ -46,7 +48,7 @@ class DeviceTableau:
 
     def __init__(self, dense: np.ndarray, n: int, m: int, flen: int, *, device=None,
                  row0: int = 0, n_global: int | None = None, log_cap: int = 1 << 16,
-                 pad_to: int = 16):
+                 pad_to: int = 16, ld_extra: int = 0):
         if not torch.cuda.is_available():
             raise RuntimeError("simplex_mi355x needs an MI355X (HIP device); there is no CPU path")
         _lib.load()
@@ -57,7 +59,7 @@ class DeviceTableau:
         self.device = torch.device(device if device is not None else "cuda")
         self.rows, self.n, self.m, self.flen, self.row0 = rows, (n if n_global is None else n_global), m, flen, row0
         self.C = C
-        self.ld = leading_dim(C, pad_to)
+        self.ld = leading_dim(C, pad_to) + ld_extra
         self.nparts = _lib.load().smx_nparts_for(rows, m)
         self.shape = [self.ld, rows, self.n, m, flen, row0, self.nparts]
         self.stream = torch.cuda.Stream(self.device)
