@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None, help="PMC summary json (default: profiles/)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the row-sharded RCCL path even at world size 1")
     return ap.parse_args()
 
 
@@ -146,7 +148,7 @@ def run_single(args):
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or args.sharded:
         from simplex_mi355x import sharded
         sharded.bench_main(args, METRIC, PEAK_HBM_GBS, cpu_baseline, load_traffic)
     else:

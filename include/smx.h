@@ -149,6 +149,13 @@ int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, i
  *   smx_shard_update(Tin, Tout, recv, ...)       pivot with the winning row
  * SMX_SHARD_HDR doubles of header precede the row in each send/recv slot. */
 #define SMX_SHARD_HDR 8
+/* One pivot = smx_shard_begin (select + pack) -> all-gather -> smx_shard_finish (merge + update);
+ * optional events (hipEvent_t, may be NULL) are recorded around the update kernel. */
+int smx_shard_begin(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                    smx_part* parts, double* send, void* stream);
+int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
+                     int64_t log_cap, void* ev_before, void* ev_after, void* stream);
 int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
                    const smx_part* parts, double* send, void* stream);
 int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,

@@ -1001,4 +1001,22 @@ int smx_shard_update(const double* Tin, double* Tout, const double* recv,
                                       recv, 0, 0, S(stream));
 }
 
+int smx_shard_begin(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                    smx_part* parts, double* send, void* stream) {
+    int err = smx_select(T, shape, parity, ctl, parts, stream);
+    if (err) return err;
+    return smx_shard_pack(T, shape, parity, ctl, parts, send, stream);
+}
+
+int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
+                     int64_t log_cap, void* ev_before, void* ev_after, void* stream) {
+    int err = smx_shard_merge(recv, nranks, shape, parity, ctl, log, log_cap, stream);
+    if (err) return err;
+    if (ev_before) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_before), S(stream));
+    err = smx_shard_update(Tin, Tout, recv, shape, parity, ctl, stream);
+    if (ev_after) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_after), S(stream));
+    return err;
+}
+
 }  // extern "C"

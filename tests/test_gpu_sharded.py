@@ -1,0 +1,82 @@
+"""GPU: the HIP shard kernels (k_select/k_pack/k_merge/k_update<kShard>) for P simulated ranks in
+one process on one device (the all-gather done by a device copy), against the unsharded C oracle,
+bit for bit.  The multi-process RCCL path itself is covered by bench.py --sharded (world 1 on the
+test box) and by the gloo tests of the same driver."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+
+
+def _simulate(T, n, m, k, P):
+    import torch
+    from simplex_mi355x.sharded import HipShardBackend, row_range
+    bes = []
+    for p in range(P):
+        lo, hi = row_range(n, p, P)
+        local = np.concatenate([T[lo:hi], T[n:n + 1]], axis=0)
+        bes.append(HipShardBackend(local, n, m, m, lo, P))
+    for _ in range(k):
+        for be in bes:
+            with be.stream_ctx():
+                be.begin()
+        torch.cuda.synchronize()
+        allsend = torch.cat([be.send for be in bes])
+        for be in bes:
+            be.recv.copy_(allsend)
+        torch.cuda.synchronize()
+        for be in bes:
+            with be.stream_ctx():
+                be.finish()
+    torch.cuda.synchronize()
+    states = [be.state() for be in bes]
+    logs = [be.log(0, s["npivots"]) for be, s in zip(bes, states)]
+    tables = [be.local_table() for be in bes]
+    full = np.concatenate([t[:-1] for t in tables] + [tables[0][-1:]], axis=0)
+    return states, logs, tables, full
+
+
+@pytest.mark.parametrize("kind,n,m,k,P", [
+    ("uniform", 1023, 1023, 80, 2),
+    ("uniform", 1001, 777, 80, 3),
+    ("uniform", 2047, 2047, 40, 8),
+    ("mixed", 700, 600, 120, 4),
+    ("degenerate", 511, 511, 120, 4),
+    ("degenerate_mixed", 300, 500, 120, 5),
+])
+def test_hip_shards_match_oracle(kind, n, m, k, P):
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    T = lp.dense_tableau(kind, 7, n, m)
+    states, logs, tables, full = _simulate(T, n, m, k, P)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    for s, lg in zip(states, logs):
+        assert s["npivots"] == done
+        assert np.array_equal(lg, log)
+    for t in tables[1:]:   # every f-row replica identical
+        assert np.array_equal(t[-1, :m].view(np.int64), tables[0][-1, :m].view(np.int64))
+    assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(full[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
+def test_hip_shards_terminal_outcome():
+    """A run that ends (optimum or error) stops identically on every rank."""
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    n, m = 40, 30
+    T = lp.dense_tableau("uniform", 2, n, m)
+    states, logs, tables, full = _simulate(T, n, m, 400, 3)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, 400)
+    assert done < 400
+    for s in states:
+        assert s["term"] and s["status"] == st and s["npivots"] == done
+    assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))
