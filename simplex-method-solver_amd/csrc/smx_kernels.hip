@@ -382,7 +382,9 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         }
     }
     const double e = prow[c];
-    const int r_local = r - row0;  // may be outside [0, rows_local): pivot row lives elsewhere
+    // local index of the pivot row, -1 when another rank owns it (never the f-row replica,
+    // whose local index rows_local may equal r - row0 for a row of the next rank)
+    const int r_local = (r >= row0 && r < row0 + rows_local) ? r - row0 : -1;
     const int R = rows_local + 1;  // + the f-row (local row rows_local)
     const int C = m + 1;
     constexpr int kChunk = kWave * 2;                  // doubles per unit

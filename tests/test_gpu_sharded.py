@@ -52,6 +52,8 @@ def _simulate(T, n, m, k, P):
     ("mixed", 700, 600, 120, 4),
     ("degenerate", 511, 511, 120, 4),
     ("degenerate_mixed", 300, 500, 120, 5),
+    ("uniform", 40, 30, 78, 3),   # step 26 pivots on row 26 = rank 2's first row: on rank 1
+                                  # r - row0 == its f-row replica's local index (regression)
 ])
 def test_hip_shards_match_oracle(kind, n, m, k, P):
     from oracle import c_oracle
