@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--size", type=int, default=16384, help="tableau is size x size (n=m=size-1)")
+    ap.add_argument("--rows", type=int, default=None, help="tableau rows R (default: --size)")
+    ap.add_argument("--cols", type=int, default=None, help="tableau columns C (default: --size)")
     ap.add_argument("--kind", default="uniform")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -65,6 +67,22 @@ def load_traffic(path, workload):
         return None if rec is None else float(rec["bytes_per_launch"])
     except Exception:
         return None
+
+
+def shape_of(args):
+    R = args.rows if args.rows else args.size
+    C = args.cols if args.cols else args.size
+    return R - 1, C - 1
+
+
+def cycle_report(n, m, log):
+    """Opt-in cycle detection over the pivots just run (host side, outside the timed region)."""
+    from simplex_mi355x.basis import BasisTracker
+    tr = BasisTracker(n, m)
+    for r, c in log:
+        if tr.pivot(int(r), int(c)):
+            break
+    return None if tr.cycle is None else {"first_step": tr.cycle[0], "period": tr.cycle[1]}
 
 
 def cpu_baseline(T, n, m, seconds):
@@ -94,10 +112,10 @@ def run_single(args):
     from simplex_mi355x import lp
     from simplex_mi355x.device import DeviceTableau
 
-    n = m = args.size - 1
+    n, m = shape_of(args)
     R, C = n + 1, m + 1
     T = lp.dense_tableau(args.kind, args.seed, n, m)
-    dev = DeviceTableau(T, n, m, m, device="cuda:0")
+    dev = DeviceTableau(T, n, m, m, device="cuda:0", log_cap=max(1 << 16, args.warmup + args.steps))
     if args.warmup:
         dev.run_timed(args.warmup)
         dev.sync_state()
@@ -107,7 +125,9 @@ def run_single(args):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     ctl = dev.sync_state()
-    valid = int(ctl["npivots"]) == args.warmup + args.steps and not ctl["term"]
+    done = int(ctl["npivots"])
+    valid = done == args.warmup + args.steps and not ctl["term"]
+    cycle = cycle_report(n, m, dev.read_log(0, done))
     bytes_per_pivot = 16.0 * R * C
     avg_upd = float(np.mean(upd_ms)) * 1e-3
     achieved = bytes_per_pivot / avg_upd / 1e9
@@ -137,6 +157,7 @@ def run_single(args):
                      "algorithmic_bytes_per_launch": bytes_per_pivot,
                      "avg_kernel_ms": avg_upd * 1e3},
         "trajectory_valid": bool(valid),
+        "basis_cycle": cycle,
     }
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(T, n, m, args.cpu_seconds)

@@ -13,7 +13,7 @@
  *                     k chained select+update pairs, no host synchronisation
  *   smx_graph_*    <- the same loop captured once as a hipGraph and replayed
  *   smx_shard_*    <- row-sharded variant for 1 process per GPU (exchange done by the caller's
- *                     RCCL all-gather between smx_shard_pack and smx_shard_merge)
+ *                     RCCL all-gather between smx_shard_begin and smx_shard_finish)
  * The reference is pure Python; it has no FFI of its own.  The Python binding a maintainer would
  * add is in INTEGRATION.md (ctypes), and simplex-method-solver_amd/simplex_mi355x/_lib.py is it.
  *
@@ -142,26 +142,31 @@ int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, i
 /* ---- row-sharded engine (one process per GPU; exchange = caller's all-gather) ----------
  * Local tableau: shape->rows constraint rows (global rows row0 .. row0+rows-1) + a replica
  * of the f-row as local row `rows`.  Per pivot:
- *   smx_select(T, shape, parity, ...)            local ratio-test partials
- *   smx_shard_pack(T, ..., send)                 header + candidate row -> send[hdr + ld]
- *   all_gather(send -> recv[P][hdr + ld])        RCCL over xGMI, by the caller
- *   smx_shard_merge(recv, P, ...)                identical decision on every rank -> ctl
- *   smx_shard_update(Tin, Tout, recv, ...)       pivot with the winning row
- * SMX_SHARD_HDR doubles of header precede the row in each send/recv slot. */
+ *   smx_select(T, shape, parity, ...)             local ratio-test / phase-1 partials
+ *   smx_shard_pack(T, ..., send)                  header + candidate rows -> send slot
+ *   all_gather(send -> recv[P][slot])             RCCL over xGMI, by the caller
+ *   smx_shard_update(Tin, Tout, recv, P, ...)     every block merges the P headers (identical
+ *                                                 decision on every rank), then pivots with the
+ *                                                 winning row read straight from recv
+ * Slot layout (doubles): [SMX_SHARD_HDR header][row A: ld][row B: ld]; header =
+ *   {local first-negative-b row | NONE, first ratio candidate | NONE, its ratio, best class,
+ *    best row, best ratio, entering column, first positive column of row B (phase 1)}.
+ * smx_shard_merge only records the selection in ctl (like smx_finalize). */
 #define SMX_SHARD_HDR 8
-/* One pivot = smx_shard_begin (select + pack) -> all-gather -> smx_shard_finish (merge + update);
- * optional events (hipEvent_t, may be NULL) are recorded around the update kernel. */
+int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
+                   const smx_part* parts, double* send, void* stream);
+int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,
+                    int32_t parity, smx_ctl* ctl, int32_t* log, int64_t log_cap, void* stream);
+int smx_shard_update(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
+                     int64_t log_cap, void* stream);
+/* One pivot = smx_shard_begin (select + pack) -> all-gather -> smx_shard_finish (update, with
+ * optional hipEvent_t records around it, may be NULL). */
 int smx_shard_begin(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                     smx_part* parts, double* send, void* stream);
 int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
                      const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
                      int64_t log_cap, void* ev_before, void* ev_after, void* stream);
-int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
-                   const smx_part* parts, double* send, void* stream);
-int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,
-                    int32_t parity, smx_ctl* ctl, int32_t* log, int64_t log_cap, void* stream);
-int smx_shard_update(const double* Tin, double* Tout, const double* recv,
-                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, void* stream);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "smx.h"
@@ -162,6 +163,95 @@ __device__ Decision decide_from_parts(const smx_ctl* ctl, const smx_part* parts,
     return d;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Every rank merges the P headers identically: phase decision (simplex.py:72-76), global arg-min
+// of the ratio test (simplex.py:105-141) and the winning row's offset in recv.  One thread.
+struct ShardDecision {
+    int status, r, c, owner;
+    int64_t off;
+};
+
+__device__ ShardDecision merge_headers(const double* __restrict__ recv, int nranks, int64_t ld,
+                                       int m, int flen) {
+    const int64_t slot = SMX_SHARD_HDR + 2 * ld;
+    int gnegb = SMX_NONE, owner_b = -1;
+    int gfirst = SMX_NONE, owner_f = -1;
+    double fv = 0.0;
+    Cand best = cand_none();
+    int owner_best = -1;
+    int c = SMX_NONE;
+    for (int p = 0; p < nranks; ++p) {
+        const double* h = recv + p * slot;
+        const int nb = (int)h[0];
+        if (nb < gnegb) {
+            gnegb = nb;
+            owner_b = p;
+        }
+        const int fi = (int)h[1];
+        if (fi < gfirst) {
+            gfirst = fi;
+            fv = h[2];
+            owner_f = p;
+        }
+        Cand o{(int)h[3], (int)h[4], h[5]};
+        if (better(o, best)) {
+            best = o;
+            owner_best = p;
+        }
+        c = (int)h[6];
+    }
+    ShardDecision d{SMX_NOT_CONVERGE, SMX_NONE, c, -1, 0};
+    if (gnegb != SMX_NONE) {                      // phase 1: the owner scanned its row
+        d.r = gnegb;
+        d.owner = owner_b;
+        d.off = owner_b * slot + SMX_SHARD_HDR + ld;
+        d.c = (int)recv[owner_b * slot + 7];
+        d.status = (d.c == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
+    } else if (c == SMX_NONE) {
+        d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
+    } else if (gfirst == SMX_NONE) {
+        d.status = SMX_NOT_CONVERGE;
+    } else if (isnan(fv)) {
+        d.status = SMX_PIVOT;
+        d.r = gfirst;
+        d.owner = owner_f;
+        d.off = owner_f * slot + SMX_SHARD_HDR;
+    } else if (best.cls >= 2) {
+        d.status = SMX_NOT_CONVERGE;
+    } else {
+        d.status = SMX_PIVOT;
+        d.r = best.idx;
+        d.owner = owner_best;
+        d.off = owner_best * slot + SMX_SHARD_HDR + ld;
+    }
+    return d;
+}
+
+// commit = false: record the selection only (smx_shard_merge, like k_finalize); commit = true:
+// also count/log the pivot or latch the terminal outcome (the update kernel's block 0).
+__device__ void publish_shard_decision(const ShardDecision& d, const double* recv,
+                                       smx_ctl* ctl, int32_t* log, int64_t log_cap, bool commit) {
+    ctl->sel_status = d.status;
+    ctl->sel_r = d.r;
+    ctl->sel_c = d.c;
+    ctl->sel_owner = d.owner;
+    ctl->reserved[0] = d.off;
+    ctl->sel_e = (d.status == SMX_PIVOT) ? recv[d.off + d.c] : 0.0;
+    if (!commit) return;
+    if (d.status == SMX_PIVOT) {
+        const int64_t k = ctl->npivots;
+        if (log_cap > 0) {
+            log[2 * (k % log_cap)] = d.r;
+            log[2 * (k % log_cap) + 1] = d.c;
+        }
+        ctl->npivots = k + 1;
+    } else {
+        ctl->term = 1;
+    }
+}
+
+// Every rank merges the P headers identically (one workgroup) and, in phase 1, scans the
+// winning row for its first positive entry (simplex.py:81-85).
 // ---------------------------------------------------------------------------------------------
 // k_reset: scan the "-b" column (rows < rows_local) and the f-row (j < fscan) of a tableau.
 __global__ __launch_bounds__(1024) void k_reset(const double* __restrict__ T, int64_t ld,
@@ -326,7 +416,22 @@ enum UpdMode { kSingle = 0, kShard = 1, kForced = 2 };
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
-template <int MODE, int U, bool NT>
+template <bool NTL>
+__device__ __forceinline__ dbl2 ld2(const double* p) {
+    if (NTL) return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
+    return *reinterpret_cast<const dbl2*>(p);
+}
+
+// One batch = U units of this wave: their rows, chunks and the 16-B tableau slices.
+template <int U>
+struct Batch {
+    int i[U], ch[U];
+    dbl2 x[U];
+    double pc[U];
+};
+
+// DIAG (timing only, never selectable in normal use): multiply by 1/e instead of dividing.
+template <int MODE, int U, bool NTS, bool NTL, bool PIPE, bool DIAG = false>
 __global__ __launch_bounds__(kUpdBlock) void k_update(
     const double* __restrict__ Tin, double* __restrict__ Tout, int64_t ld, int rows_local,
     int n, int m, int flen, int fscan, int row0, int parity, smx_ctl* __restrict__ ctl,
@@ -335,56 +440,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     __shared__ int s_dec[3];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    int r, c;
-    const double* prow;
-    if (MODE == kForced) {
-        r = forced_r;
-        c = forced_c;
-        prow = Tin + (int64_t)r * ld;
-    } else {
-        if (ctl->term) return;
-        if (MODE == kSingle) {
-            if (tid < kWave) {
-                const Decision d = decide_from_parts(ctl, parts, nparts, parity, n, m, flen);
-                if (tid == 0) {
-                    s_dec[0] = d.status;
-                    s_dec[1] = d.r;
-                    s_dec[2] = d.c;
-                    if (blockIdx.x == 0) {
-                        ctl->sel_status = d.status;
-                        ctl->sel_r = d.r;
-                        ctl->sel_c = d.c;
-                        if (d.status == SMX_PIVOT) {
-                            ctl->sel_e = Tin[(int64_t)d.r * ld + d.c];
-                            const int64_t k = ctl->npivots;
-                            if (log_cap > 0) {
-                                log[2 * (k % log_cap)] = d.r;
-                                log[2 * (k % log_cap) + 1] = d.c;
-                            }
-                            ctl->npivots = k + 1;
-                        } else {
-                            ctl->term = 1;
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            if (s_dec[0] != SMX_PIVOT) return;
-            r = __builtin_amdgcn_readfirstlane(s_dec[1]);
-            c = __builtin_amdgcn_readfirstlane(s_dec[2]);
-            prow = Tin + (int64_t)r * ld;
-        } else {  // kShard: k_merge already decided and published into ctl
-            if (ctl->sel_status != SMX_PIVOT) return;
-            r = __builtin_amdgcn_readfirstlane(ctl->sel_r);
-            c = __builtin_amdgcn_readfirstlane(ctl->sel_c);
-            const int64_t off = ctl->reserved[0];
-            prow = recv + off;
-        }
-    }
-    const double e = prow[c];
-    // local index of the pivot row, -1 when another rank owns it (never the f-row replica,
-    // whose local index rows_local may equal r - row0 for a row of the next rank)
-    const int r_local = (r >= row0 && r < row0 + rows_local) ? r - row0 : -1;
+    if (MODE != kForced && ctl->term) return;
     const int R = rows_local + 1;  // + the f-row (local row rows_local)
     const int C = m + 1;
     constexpr int kChunk = kWave * 2;                  // doubles per unit
@@ -395,20 +451,14 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     // unit u = i * nchunks + ch; advancing u by NW advances (i, ch) by (qs, rs)
     const int qs = NW / nchunks, rs = NW % nchunks;
     int i_cur = w / nchunks, ch_cur = w % nchunks;
-    int ch_pr = -1;
-    dbl2 pr = dbl2{0.0, 0.0};
-    const int negslot = parity ^ 1;
-    int lb = SMX_NONE;   // fused next-step scan: first row with new b < 0 (this lane)
-    int lf = SMX_NONE;   // fused next-step scan: first f-row column with new f < 0 (this lane)
 
-    for (int64_t u = w; u < units; u += (int64_t)U * NW) {
-        int iu[U], chu[U];
-        dbl2 x[U];
-        double pc[U];
+    // address part of a batch: independent of the pivot, so the first batch's loads are in
+    // flight while the selection decision below is still being reduced
+    auto fetch = [&](Batch<U>& b) {
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            iu[k] = i_cur;
-            chu[k] = ch_cur;
+            b.i[k] = i_cur;
+            b.ch[k] = ch_cur;
             ch_cur += rs;
             i_cur += qs;
             if (ch_cur >= nchunks) {
@@ -418,38 +468,108 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         }
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            x[k] = dbl2{0.0, 0.0};
-            pc[k] = 0.0;
-            if (iu[k] < R) {
-                const double* src = Tin + (int64_t)iu[k] * ld;
-                const int j = chu[k] * kChunk + 2 * lane;
-                pc[k] = src[c];
-                if (j < C) x[k] = *reinterpret_cast<const dbl2*>(src + j);
+            b.x[k] = dbl2{0.0, 0.0};
+            const int j = b.ch[k] * kChunk + 2 * lane;
+            if (b.i[k] < R && j < C) b.x[k] = ld2<NTL>(Tin + (int64_t)b.i[k] * ld + j);
+        }
+    };
+    Batch<U> cur;
+    fetch(cur);
+
+    int r, c;
+    const double* prow;
+    if (MODE == kForced) {
+        r = forced_r;
+        c = forced_c;
+        prow = Tin + (int64_t)r * ld;
+    } else if (MODE == kSingle) {
+        if (tid < kWave) {
+            const Decision d = decide_from_parts(ctl, parts, nparts, parity, n, m, flen);
+            if (tid == 0) {
+                s_dec[0] = d.status;
+                s_dec[1] = d.r;
+                s_dec[2] = d.c;
+                if (blockIdx.x == 0) {
+                    ctl->sel_status = d.status;
+                    ctl->sel_r = d.r;
+                    ctl->sel_c = d.c;
+                    if (d.status == SMX_PIVOT) {
+                        ctl->sel_e = Tin[(int64_t)d.r * ld + d.c];
+                        const int64_t k = ctl->npivots;
+                        if (log_cap > 0) {
+                            log[2 * (k % log_cap)] = d.r;
+                            log[2 * (k % log_cap) + 1] = d.c;
+                        }
+                        ctl->npivots = k + 1;
+                    } else {
+                        ctl->term = 1;
+                    }
+                }
             }
         }
+        __syncthreads();
+        if (s_dec[0] != SMX_PIVOT) return;
+        r = __builtin_amdgcn_readfirstlane(s_dec[1]);
+        c = __builtin_amdgcn_readfirstlane(s_dec[2]);
+        prow = Tin + (int64_t)r * ld;
+    } else {  // kShard: every block merges the P gathered headers itself (nparts = P)
+        __shared__ int64_t s_off;
+        if (tid == 0) {
+            const ShardDecision d = merge_headers(recv, nparts, ld, m, flen);
+            s_dec[0] = d.status;
+            s_dec[1] = d.r;
+            s_dec[2] = d.c;
+            s_off = d.off;
+            if (blockIdx.x == 0) publish_shard_decision(d, recv, ctl, log, log_cap, true);
+        }
+        __syncthreads();
+        if (s_dec[0] != SMX_PIVOT) return;
+        r = __builtin_amdgcn_readfirstlane(s_dec[1]);
+        c = __builtin_amdgcn_readfirstlane(s_dec[2]);
+        prow = recv + s_off;
+    }
+    const double e = prow[c];
+    // local index of the pivot row, -1 when another rank owns it (never the f-row replica,
+    // whose local index rows_local may equal r - row0 for a row of the next rank)
+    const int r_local = (r >= row0 && r < row0 + rows_local) ? r - row0 : -1;
+    int ch_pr = -1;
+    dbl2 pr = dbl2{0.0, 0.0};
+    const int negslot = parity ^ 1;
+    int lb = SMX_NONE;   // fused next-step scan: first row with new b < 0 (this lane)
+    int lf = SMX_NONE;   // fused next-step scan: first f-row column with new f < 0 (this lane)
+
+    for (int64_t u = w; u < units; u += (int64_t)U * NW) {
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            cur.pc[k] = (cur.i[k] < R) ? Tin[(int64_t)cur.i[k] * ld + c] : 0.0;
+        Batch<U> nxt;
+        if (PIPE && u + (int64_t)U * NW < units) fetch(nxt);
 #pragma unroll
         for (int k = 0; k < U; ++k) {
-            const int i = iu[k];
+            const int i = cur.i[k];
             if (i >= R) continue;
-            const int j = chu[k] * kChunk + 2 * lane;
-            if (chu[k] != ch_pr) {
-                ch_pr = chu[k];
+            const int j = cur.ch[k] * kChunk + 2 * lane;
+            if (cur.ch[k] != ch_pr) {
+                ch_pr = cur.ch[k];
                 pr = (j < C) ? *reinterpret_cast<const dbl2*>(prow + j) : dbl2{0.0, 0.0};
             }
             dbl2 o;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int jj = j + h;
-                const double xv = x[k][h];
+                const double xv = cur.x[k][h];
                 double num;
                 if (i == r_local) {
                     num = (jj == c) ? 1.0 : -xv;
                 } else {
                     const double a = xv * e;
-                    const double b = pr[h] * pc[k];
+                    const double b = pr[h] * cur.pc[k];
                     num = (jj == c) ? xv : (a - b);
                 }
-                o[h] = num / e;
+                if (DIAG)
+                    o[h] = num * (1.0 / e);
+                else
+                    o[h] = num / e;
                 if (MODE != kForced && jj < C) {
                     if (i < rows_local) {
                         if (jj == m && o[h] < 0.0) lb = min(lb, row0 + i);
@@ -460,11 +580,16 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
             }
             if (j < C) {
                 double* dst = Tout + (int64_t)i * ld + j;
-                if (NT)
+                if (NTS)
                     __builtin_nontemporal_store(o, reinterpret_cast<dbl2*>(dst));
                 else
                     *reinterpret_cast<dbl2*>(dst) = o;
             }
+        }
+        if (PIPE) {
+            cur = nxt;
+        } else if (u + (int64_t)U * NW < units) {
+            fetch(cur);
         }
     }
     if (MODE != kForced) {
@@ -484,6 +609,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
 //   hdr[2] its ratio v
 //   hdr[3] best class, hdr[4] best row (global), hdr[5] best v -> row B = best row (phase 2)
 //   hdr[6] entering column c (replicated f-row => same on every rank)
+//   hdr[7] phase 1: first column j < m with row B [j] > 0 (computed by the row's owner), or NONE
 __global__ __launch_bounds__(kUpdBlock) void k_pack(const double* __restrict__ T, int64_t ld,
                                                      int rows, int m, int row0, int parity,
                                                      const smx_ctl* __restrict__ ctl,
@@ -499,6 +625,11 @@ __global__ __launch_bounds__(kUpdBlock) void k_pack(const double* __restrict__ T
         const int c = ctl->negf[parity];
         First f{SMX_NONE, 0.0};
         Cand b = cand_none();
+        int p1 = SMX_NONE;   // phase 1: first column with T[negb][j] > 0 (simplex.py:81-85)
+        if (negb != SMX_NONE) {
+            for (int k = tid; k < nparts; k += kWave) p1 = min(p1, parts[k].p1col);
+            p1 = wave_min_int(p1);
+        }
         if (negb == SMX_NONE && c != SMX_NONE) {
             for (int k = tid; k < nparts; k += kWave) {
                 const smx_part p = parts[k];
@@ -529,7 +660,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_pack(const double* __restrict__ T
                 send[4] = (double)b.idx;
                 send[5] = b.v;
                 send[6] = (double)c;
-                send[7] = 0.0;
+                send[7] = (double)p1;
             }
         }
     }
@@ -544,115 +675,14 @@ __global__ __launch_bounds__(kUpdBlock) void k_pack(const double* __restrict__ T
     }
 }
 
-// Every rank merges the P headers identically (one workgroup) and, in phase 1, scans the
-// winning row for its first positive entry (simplex.py:81-85).
-__global__ __launch_bounds__(1024) void k_merge(const double* __restrict__ recv, int nranks,
-                                                int64_t ld, int n, int m, int flen,
-                                                smx_ctl* __restrict__ ctl,
-                                                int32_t* __restrict__ log, int64_t log_cap) {
-    __shared__ int s_dec[4];
-    __shared__ int64_t s_off;
-    __shared__ int s_w[16];
-    const int tid = threadIdx.x;
-    const int64_t slot = SMX_SHARD_HDR + 2 * ld;
-    if (ctl->term) return;
-    if (tid == 0) {
-        int gnegb = SMX_NONE, owner_b = -1;
-        int gfirst = SMX_NONE, owner_f = -1;
-        double fv = 0.0;
-        Cand best = cand_none();
-        int owner_best = -1;
-        int c = SMX_NONE;
-        for (int p = 0; p < nranks; ++p) {
-            const double* h = recv + p * slot;
-            const int nb = (int)h[0];
-            if (nb < gnegb) {
-                gnegb = nb;
-                owner_b = p;
-            }
-            const int fi = (int)h[1];
-            if (fi < gfirst) {
-                gfirst = fi;
-                fv = h[2];
-                owner_f = p;
-            }
-            Cand o{(int)h[3], (int)h[4], h[5]};
-            if (better(o, best)) {
-                best = o;
-                owner_best = p;
-            }
-            c = (int)h[6];
-        }
-        int status, r = SMX_NONE;
-        int64_t off = 0;
-        if (gnegb != SMX_NONE) {
-            status = -1;  // phase 1: column chosen below
-            r = gnegb;
-            off = owner_b * slot + SMX_SHARD_HDR + ld;
-        } else if (c == SMX_NONE) {
-            status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
-        } else if (gfirst == SMX_NONE) {
-            status = SMX_NOT_CONVERGE;
-        } else if (isnan(fv)) {
-            status = SMX_PIVOT;
-            r = gfirst;
-            off = owner_f * slot + SMX_SHARD_HDR;
-        } else if (best.cls >= 2) {
-            status = SMX_NOT_CONVERGE;
-        } else {
-            status = SMX_PIVOT;
-            r = best.idx;
-            off = owner_best * slot + SMX_SHARD_HDR + ld;
-        }
-        s_dec[0] = status;
-        s_dec[1] = r;
-        s_dec[2] = c;
-        s_dec[3] = (gnegb != SMX_NONE) ? owner_b : (status == SMX_PIVOT ? (int)(off / slot) : -1);
-        s_off = off;
-    }
-    __syncthreads();
-    int status = s_dec[0];
-    int c = s_dec[2];
-    if (status == -1) {
-        const double* prow = recv + s_off;
-        int p1 = SMX_NONE;
-        for (int j = tid; j < m; j += blockDim.x) {
-            if (prow[j] > 0.0) {
-                p1 = j;
-                break;
-            }
-        }
-        p1 = wave_min_int(p1);
-        if ((tid & 63) == 0) s_w[tid >> 6] = p1;
-        __syncthreads();
-        if (tid == 0) {
-            for (int w = 1; w < (int)(blockDim.x >> 6); ++w) p1 = min(p1, s_w[w]);
-            s_dec[0] = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
-            s_dec[2] = p1;
-        }
-        __syncthreads();
-        status = s_dec[0];
-        c = s_dec[2];
-    }
-    if (tid == 0) {
-        const int r = s_dec[1];
-        ctl->sel_status = status;
-        ctl->sel_r = r;
-        ctl->sel_c = c;
-        ctl->sel_owner = s_dec[3];
-        ctl->reserved[0] = s_off;
-        if (status == SMX_PIVOT) {
-            ctl->sel_e = recv[s_off + c];
-            const int64_t k = ctl->npivots;
-            if (log_cap > 0) {
-                log[2 * (k % log_cap)] = r;
-                log[2 * (k % log_cap) + 1] = c;
-            }
-            ctl->npivots = k + 1;
-        } else {
-            ctl->term = 1;
-        }
-    }
+__global__ __launch_bounds__(kWave) void k_merge(const double* __restrict__ recv, int nranks,
+                                                 int64_t ld, int n, int m, int flen,
+                                                 smx_ctl* __restrict__ ctl,
+                                                 int32_t* __restrict__ log, int64_t log_cap) {
+    (void)n;
+    if (ctl->term || threadIdx.x != 0) return;
+    const ShardDecision d = merge_headers(recv, nranks, ld, m, flen);
+    publish_shard_decision(d, recv, ctl, log, log_cap, false);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -687,13 +717,17 @@ int launch_select(const double* T, const smx_shape& s, int parity, smx_ctl* ctl,
 
 // ---- update-kernel variants (rows per unit TR, doubles per lane VEC, non-temporal stores) -----
 struct UpdVariant {
-    int u, nt;
+    int u, nts, ntl, pipe;
 };
-constexpr UpdVariant kVariants[] = {{1, 0}, {2, 0}, {4, 0}, {8, 0}, {1, 1}, {2, 1}, {4, 1}, {8, 1}};
+constexpr UpdVariant kVariants[] = {{2, 1, 0, 0}, {2, 1, 1, 0}, {2, 1, 0, 1}, {2, 1, 1, 1},
+                                    {1, 1, 0, 1}, {1, 1, 1, 1}, {4, 1, 0, 0}, {4, 1, 0, 1},
+                                    {2, 0, 0, 0}, {1, 1, 0, 0},
+                                    // diagnostics (reciprocal multiply: timing only)
+                                    {2, 1, 1, 0}, {1, 1, 1, 1}};
+constexpr int kFirstDiagVariant = 10;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-// Defaults from tools/tune_update.py on MI355X at 16384^2 (profiles/r01_tune_sweep.jsonl):
-// U = 2 loads in flight per lane, non-temporal stores, 5 resident blocks (20 waves) per CU.
-int g_variant = 5;        // smx_tune_set overrides
+// Defaults from tools/tune_update.py on MI355X at 16384^2 (profiles/r01_tune_sweep*.jsonl).
+int g_variant = 1;        // U=2, nt stores + nt loads, 5 blocks/CU; smx_tune_set overrides
 int g_blocks_per_cu = 0;  // 0: kDefaultBpc, capped by the occupancy API (see blocks_per_cu)
 constexpr int kDefaultBpc = 5;
 
@@ -703,14 +737,18 @@ using UpdFn = void (*)(const double*, double*, int64_t, int, int, int, int, int,
 template <int MODE>
 UpdFn upd_fn(int v) {
     switch (v) {
-        case 0: return k_update<MODE, 1, false>;
-        case 1: return k_update<MODE, 2, false>;
-        case 2: return k_update<MODE, 4, false>;
-        case 3: return k_update<MODE, 8, false>;
-        case 4: return k_update<MODE, 1, true>;
-        case 5: return k_update<MODE, 2, true>;
-        case 6: return k_update<MODE, 4, true>;
-        default: return k_update<MODE, 8, true>;
+        case 0: return k_update<MODE, 2, true, false, false>;
+        case 1: return k_update<MODE, 2, true, true, false>;
+        case 2: return k_update<MODE, 2, true, false, true>;
+        case 3: return k_update<MODE, 2, true, true, true>;
+        case 4: return k_update<MODE, 1, true, false, true>;
+        case 5: return k_update<MODE, 1, true, true, true>;
+        case 6: return k_update<MODE, 4, true, false, false>;
+        case 7: return k_update<MODE, 4, true, false, true>;
+        case 8: return k_update<MODE, 2, false, false, false>;
+        case 9: return k_update<MODE, 1, true, false, false>;
+        case 10: return k_update<MODE, 2, true, true, false, true>;
+        default: return k_update<MODE, 1, true, true, true, true>;
     }
 }
 
@@ -836,6 +874,10 @@ int smx_nparts_for(int32_t rows, int32_t m) { return nparts_for(rows, m); }
 
 int smx_tune_set(int32_t variant, int32_t blocks_per_cu_override) {
     if (variant >= kNumVariants) return (int)hipErrorInvalidValue;
+    if (variant >= kFirstDiagVariant) {   // wrong-bits timing variants: explicit opt-in only
+        const char* env = getenv("SMX_ALLOW_DIAG");
+        if (!env || env[0] != '1') return (int)hipErrorInvalidValue;
+    }
     if (variant >= 0) g_variant = variant;
     if (blocks_per_cu_override >= 0) g_blocks_per_cu = blocks_per_cu_override;
     return 0;
@@ -848,7 +890,8 @@ int smx_tune_get(int32_t* variant, int32_t* blocks_per_cu_override, int32_t* nva
     if (nvariants) *nvariants = kNumVariants;
     if (units_in_flight) *units_in_flight = kVariants[g_variant].u;
     if (vec) *vec = 2;
-    if (nt) *nt = kVariants[g_variant].nt;
+    if (nt) *nt = kVariants[g_variant].nts | (kVariants[g_variant].ntl << 1) |
+                  (kVariants[g_variant].pipe << 2);
     return 0;
 }
 
@@ -991,15 +1034,18 @@ int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,
                     int32_t parity, smx_ctl* ctl, int32_t* log, int64_t log_cap, void* stream) {
     (void)parity;
     if (!shape_ok(shape) || nranks < 1) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_merge, dim3(1), dim3(1024), 0, S(stream), recv, nranks, shape->ld,
+    hipLaunchKernelGGL(k_merge, dim3(1), dim3(kWave), 0, S(stream), recv, nranks, shape->ld,
                        shape->n, shape->m, shape->flen, ctl, log, log_cap);
     return (int)hipGetLastError();
 }
 
-int smx_shard_update(const double* Tin, double* Tout, const double* recv,
-                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, void* stream) {
-    if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
-    return launch_update_mode<kShard>(Tin, Tout, *shape, parity & 1, ctl, nullptr, nullptr, 0,
+int smx_shard_update(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                     const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
+                     int64_t log_cap, void* stream) {
+    if (!shape_ok(shape) || Tin == Tout || nranks < 1) return (int)hipErrorInvalidValue;
+    smx_shape sh = *shape;
+    sh.nparts = nranks;   // the update kernel's partial count is the rank count in shard mode
+    return launch_update_mode<kShard>(Tin, Tout, sh, parity & 1, ctl, nullptr, log, log_cap,
                                       recv, 0, 0, S(stream));
 }
 
@@ -1013,10 +1059,9 @@ int smx_shard_begin(const double* T, const smx_shape* shape, int32_t parity, smx
 int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
                      const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
                      int64_t log_cap, void* ev_before, void* ev_after, void* stream) {
-    int err = smx_shard_merge(recv, nranks, shape, parity, ctl, log, log_cap, stream);
-    if (err) return err;
     if (ev_before) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_before), S(stream));
-    err = smx_shard_update(Tin, Tout, recv, shape, parity, ctl, stream);
+    const int err = smx_shard_update(Tin, Tout, recv, nranks, shape, parity, ctl, log, log_cap,
+                                     stream);
     if (ev_after) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_after), S(stream));
     return err;
 }

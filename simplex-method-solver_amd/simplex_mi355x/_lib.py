@@ -81,7 +81,7 @@ def load():
         "smx_update_forced": ([vp, vp, sp, i32, i32, vp], ctypes.c_int),
         "smx_shard_pack": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_merge": ([vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
-        "smx_shard_update": ([vp, vp, vp, sp, i32, vp, vp], ctypes.c_int),
+        "smx_shard_update": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_shard_begin": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp, vp, vp], ctypes.c_int),
     }

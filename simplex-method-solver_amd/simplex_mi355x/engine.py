@@ -25,6 +25,7 @@ import copy
 import numpy as np
 
 from . import _lib
+from .basis import BasisTracker
 from .device import DeviceTableau
 
 MESSAGES = {_lib.INCORRECT: "incorrect system",                  # simplex.py:89
@@ -91,6 +92,8 @@ class SimplexMethod:
         self._pristine = True
         self.pivot_log: list[tuple[int, int]] = []
         self.status = "ready"
+        self.cycle = None          # (first step of a repeated basis, period) when detected
+        self._tracker = None
 
     # ---------------------------------------------------------------- state views --------
     @property
@@ -188,9 +191,23 @@ class SimplexMethod:
             return
         self._apply(r, c)
 
-    def get_solution(self, max_pivots=None):
-        """simplex.py:179-199.  ``max_pivots`` (default: none, as in the reference) bounds
-        cycling inputs; when it is hit the list simply ends and ``status == 'cap'``."""
+    def _track(self, r, c, detect_cycles):
+        """Feed a pivot to the opt-in cycle detector; True when the basis has repeated."""
+        if not detect_cycles:
+            return False
+        if self._tracker is None:
+            self._tracker = BasisTracker(self.n, self.m)
+            for rr, cc in self.pivot_log[:-1]:
+                self._tracker.pivot(rr, cc)
+        if self._tracker.pivot(r, c) is not None:
+            self.cycle = self._tracker.cycle
+            return True
+        return False
+
+    def get_solution(self, max_pivots=None, detect_cycles=False):
+        """simplex.py:179-199.  Opt-in additions (defaults = the reference's behaviour):
+        ``max_pivots`` bounds the loop (the list ends, ``status == 'cap'``); ``detect_cycles``
+        ends it when the basis repeats (``status == 'cycle'``, ``self.cycle``)."""
         result = []
         result.append(Info(self.row, self.column, self.table, None, None, 0, 0, 0))
         done = 0
@@ -214,6 +231,9 @@ class SimplexMethod:
             x1, x2 = self.find_optimum()
             result.append(Info(self.row, self.column, self.table, None, None, x1, x2,
                                self.f(x1, x2)))
+            if self._track(i, j, detect_cycles):
+                self.status = "cycle"
+                break
         return result
 
     # ---------------------------------------------------------------- additions ----------
@@ -224,14 +244,16 @@ class SimplexMethod:
             self._apply(res[1], res[2])
         return res
 
-    def solve(self, record_history=True, max_pivots=None, chunk=256, graph=True):
+    def solve(self, record_history=True, max_pivots=None, chunk=256, graph=True,
+              detect_cycles=False):
         """``get_solution`` (record_history=True) or the chained fast path: pivots run on the
         device in chunks of ``chunk`` with no host synchronisation inside a chunk; returns
-        ``[Info(initial, i/j of the first pivot), Info(final)]`` plus a trailing ``Error``."""
+        ``[Info(initial, i/j of the first pivot), Info(final)]`` plus a trailing ``Error``.
+        ``detect_cycles`` stops at the end of the chunk in which the basis first repeats."""
         if record_history:
-            return self.get_solution(max_pivots=max_pivots)
+            return self.get_solution(max_pivots=max_pivots, detect_cycles=detect_cycles)
         if self.flen not in (self.m, self.m + 1) or self.flen < 2:
-            return self._solve_stepwise(max_pivots)
+            return self._solve_stepwise(max_pivots, detect_cycles)
         first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
         start = self.pivots
         budget = float("inf") if max_pivots is None else int(max_pivots)
@@ -243,14 +265,19 @@ class SimplexMethod:
             dev.run(k, graph=graph and k == chunk)
             ctl = dev.sync_state()
             done = int(ctl["npivots"])
+            cycled = False
             for r, c in dev.read_log(before, done):
                 r, c = int(r), int(c)
                 self.row[c], self.column[r] = self.column[r], self.row[c]
                 self.pivot_log.append((r, c))
+                cycled = self._track(r, c, detect_cycles) or cycled
             if done > 0:
                 self._pristine = False
             if ctl["term"]:
                 status = int(ctl["sel_status"])
+                break
+            if cycled:
+                status = "cycle"
                 break
         out = [first]
         if self.pivots > start:
@@ -259,6 +286,8 @@ class SimplexMethod:
         out.append(Info(self.row, self.column, self.table, None, None, x1, x2, self.f(x1, x2)))
         if status is None:
             self.status = "cap"
+        elif status == "cycle":
+            self.status = "cycle"
         elif status == _lib.OPTIMUM:
             self.status = "optimum"
         elif status in MESSAGES:
@@ -268,7 +297,7 @@ class SimplexMethod:
             raise RuntimeError(f"unexpected terminal status {status}")
         return out
 
-    def _solve_stepwise(self, max_pivots):
+    def _solve_stepwise(self, max_pivots, detect_cycles=False):
         first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
         out = [first]
         done = 0
@@ -288,7 +317,12 @@ class SimplexMethod:
                 first.i, first.j = i, j
             self._apply(i, j)
             done += 1
-        self.status = "optimum" if (max_pivots is None or done < max_pivots) else "cap"
+            if self._track(i, j, detect_cycles):
+                break
+        if self.cycle is not None and detect_cycles:
+            self.status = "cycle"
+        else:
+            self.status = "optimum" if (max_pivots is None or done < max_pivots) else "cap"
         x1, x2 = self.find_optimum()
         out.append(Info(self.row, self.column, self.table, None, None, x1, x2, self.f(x1, x2)))
         return out

@@ -165,12 +165,15 @@ def shard_merge(recv: Tensor, ctl: Tensor, log: Tensor, shape: list[int], parity
                "smx_shard_merge")
 
 
-@torch.library.custom_op("smx::shard_update", mutates_args=("tout",))
-def shard_update(tin: Tensor, tout: Tensor, recv: Tensor, ctl: Tensor, shape: list[int],
-                 parity: int) -> None:
-    """Pivot the local rows (and the f-row replica) with the winning row from recv."""
+@torch.library.custom_op("smx::shard_update", mutates_args=("tout", "ctl", "log"))
+def shard_update(tin: Tensor, tout: Tensor, recv: Tensor, ctl: Tensor, log: Tensor,
+                 shape: list[int], parity: int, nranks: int) -> None:
+    """Merge the gathered headers (identically on every rank) and pivot the local rows and the
+    f-row replica with the winning row from recv."""
     _table_ok(tin, shape, "tin")
     _table_ok(tout, shape, "tout")
+    _bytes_ok(recv, nranks * shard_slot(int(shape[0])) * 8, "recv")
     sh = make_shape(shape)
-    _lib.check(_lib.load().smx_shard_update(_ptr(tin), _ptr(tout), _ptr(recv), ctypes.byref(sh),
-                                            parity, _ptr(ctl), _stream()), "smx_shard_update")
+    _lib.check(_lib.load().smx_shard_update(_ptr(tin), _ptr(tout), _ptr(recv), nranks,
+                                            ctypes.byref(sh), parity, _ptr(ctl), _ptr(log),
+                                            _log_cap(log), _stream()), "smx_shard_update")

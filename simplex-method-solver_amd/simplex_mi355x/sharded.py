@@ -119,19 +119,21 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"),
                  ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")):
         os.environ.setdefault(k, v)   # plain `python bench.py --sharded` = a 1-rank job
-    if not dist.is_initialized():
-        dist.init_process_group("nccl")
-    rank, world = dist.get_rank(), dist.get_world_size()
-    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    local_rank = int(os.environ["LOCAL_RANK"])
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    n = m = args.size - 1
-    R, C = n + 1, m + 1
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=device)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    R = args.rows if getattr(args, "rows", None) else args.size
+    C = args.cols if getattr(args, "cols", None) else args.size
+    n, m = R - 1, C - 1
     lo, hi = row_range(n, rank, world)
     local = np.zeros((hi - lo + 1, m + 1), dtype=np.float64)
     local[:-1] = lp.dense_rows(args.kind, args.seed, n, m, lo, hi)
     local[-1, :m] = lp.objective(args.kind, args.seed, m)
-    be = HipShardBackend(local, n, m, m, lo, world, device=device)
+    be = HipShardBackend(local, n, m, m, lo, world, device=device,
+                         log_cap=max(1 << 16, args.warmup + args.steps))
     del local
     solver = ShardedSolver(be)
     if args.warmup:
@@ -153,6 +155,14 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     st = be.state()
+    cycle = None
+    if rank == 0:
+        from .basis import BasisTracker
+        tr = BasisTracker(n, m)
+        for r, c in be.log(0, st["npivots"]):
+            if tr.pivot(int(r), int(c)):
+                cycle = {"first_step": tr.cycle[0], "period": tr.cycle[1]}
+                break
     upd_ms = np.array([a.elapsed_time(b) for a, b in evs], dtype=np.float64)
     stats = torch.tensor([elapsed, float(upd_ms.mean()),
                           float(st["npivots"] == args.warmup + args.steps and not st["term"])],
@@ -184,7 +194,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
                     "on the host and uploads it to its HBM before timing (no dataset)",
             "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
                        "parallelism": f"row-shard x{world} (1 all-gather per pivot, RCCL)",
-                       "rows_per_rank": hi - lo, "kernels_per_pivot": 4,
+                       "rows_per_rank": hi - lo, "kernels_per_pivot": 3,
                        "collectives_per_pivot": 1},
             "hbm_gbs_per_pivot": 16.0 * R * C / (wall / args.steps) / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak_gbs, "unit": "GB/s",
@@ -194,6 +204,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
                          "avg_kernel_ms": avg_upd * 1e3,
                          "max_rank_avg_kernel_ms": float(mx[1])},
             "trajectory_valid": bool(mn[2] > 0.5),
+            "basis_cycle": cycle,
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)

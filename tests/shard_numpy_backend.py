@@ -1,7 +1,8 @@
 """CPU stand-in for HipShardBackend, used only by the gloo tests of the sharded protocol.
 
 It mirrors the HIP kernels' semantics and buffer layouts exactly (k_select + k_pack ->
-smx_shard_begin, k_merge + k_update<kShard> -> smx_shard_finish; include/smx.h), so the
+smx_shard_begin, k_update<kShard> with its in-kernel header merge -> smx_shard_finish;
+include/smx.h), so the
 Python driver (simplex_mi355x.sharded.ShardedSolver) and its collective run unchanged over
 gloo on CPU tensors.  The arithmetic follows oracle/numpy_oracle.py (simplex.py:149-177).
 """
@@ -77,8 +78,12 @@ class NumpyShardBackend:
                     x = (cls, self.row0 + int(i), float(vi))
                     if _better(x, best):
                         best = x
+        p1 = NONE   # phase 1: the owner scans its own first-negative-b row (simplex.py:81-85)
+        if negb != NONE:
+            pos = np.flatnonzero(self.T[negb - self.row0, :self.m] > 0)
+            p1 = int(pos[0]) if pos.size else NONE
         send = self.send.numpy()
-        send[:HDR] = [negb, first, first_v, best[0], best[1], best[2], c, 0.0]
+        send[:HDR] = [negb, first, first_v, best[0], best[1], best[2], c, p1]
         if first != NONE and np.isnan(first_v):
             send[HDR:HDR + self.ld] = self.T[first - self.row0]
         rb = negb if negb != NONE else (best[1] if best[0] < 3 else NONE)
@@ -107,11 +112,8 @@ class NumpyShardBackend:
         r, row = NONE, None
         if gnegb != NONE:
             r, row = gnegb, recv[owner_b, HDR + self.ld:HDR + 2 * self.ld]
-            pos = np.flatnonzero(row[:self.m] > 0)
-            if pos.size:
-                status, c = PIVOT, int(pos[0])
-            else:
-                status, c = INCORRECT, NONE
+            c = int(recv[owner_b, 7])
+            status = PIVOT if c != NONE else INCORRECT
         elif c == NONE:
             status = FSHORT if self.flen < self.m else OPTIMUM
         elif gfirst == NONE:

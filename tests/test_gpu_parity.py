@@ -4,6 +4,7 @@ fixtures and the pinned CPU oracle.  Bit-exact: every table compared as int64 bi
 """
 from __future__ import annotations
 
+import os
 import numpy as np
 import pytest
 
@@ -212,3 +213,39 @@ def test_full_size_prefix_vs_oracle(n, m, k):
     got = dev.download()
     assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
     assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
+# ----------------------------------------------------------------------------------------------
+# 6. opt-in cycle detection on a cycling fixture (the reference itself loops forever here)
+def test_solve_detects_basis_cycle():
+    import simplex
+    rec = load("degenerate.json")[0]
+    cons, func = dec_input(rec["input"])
+    for history in (True, False):
+        sm = simplex.SimplexMethod([list(r) for r in cons], list(func))
+        sm.solve(record_history=history, max_pivots=500, chunk=4, detect_cycles=True)
+        assert sm.status == "cycle" and sm.cycle == (3, 2)
+        exp = [(s["i"], s["j"]) for s in rec["steps"][:len(sm.pivot_log)]]
+        assert sm.pivot_log == exp
+
+
+# ----------------------------------------------------------------------------------------------
+# 7. bench.py itself (single path and the RCCL sharded path at world size 1)
+def _bench_json(cmd):
+    import json
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable] + cmd, capture_output=True, text=True, timeout=600,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+def test_bench_single_and_sharded_paths():
+    for extra in ([], ["--sharded"]):
+        rec = _bench_json(["bench.py", "--size", "2048", "--steps", "20", "--warmup", "2",
+                           "--no-cpu-baseline"] + extra)
+        assert rec["trajectory_valid"] and rec["n_gpus"] == 1 and rec["value"] > 0
+        assert rec["roofline"]["bound"] == "hbm" and 0 < rec["roofline"]["frac"] < 1
