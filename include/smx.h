@@ -47,8 +47,11 @@ extern "C" {
 #define SMX_IDLE 5          /* no selection made yet                                         */
 
 #define SMX_NONE 0x7f7f7f7f /* "no index" sentinel (memset byte 0x7f)                        */
+#define SMX_ABSENT ((int32_t)0x80000000) /* label position code: label does not exist      */
 
-/* Device control block (caller allocates sizeof(smx_ctl) bytes of device memory). */
+/* Device control block (caller allocates sizeof(smx_ctl) bytes of device memory).
+ * Fields indexed [parity] are double-buffered: step s reads slot s&1 and its update kernel writes
+ * slot (s+1)&1, so no kernel ever reads a word another block of the same launch is writing. */
 typedef struct smx_ctl {
     int32_t negb[2];    /* per parity slot: first row i < n with T[i][m] < 0 (global index)  */
     int32_t negf[2];    /* per parity slot: first j < min(m, flen) with f[j] < 0             */
@@ -60,7 +63,11 @@ typedef struct smx_ctl {
     int64_t npivots;    /* pivots applied since smx_reset(..., clear_count=1)                 */
     int32_t sel_owner;  /* sharded: rank whose candidate row is the pivot row                 */
     int32_t pad0;
-    int64_t reserved[9];    /* reserved[0]: sharded, offset (in doubles) of the pivot row in recv */
+    int64_t shard_off;  /* sharded: offset (doubles) of the pivot row in the receive buffer   */
+    int32_t xpos[2][2]; /* [parity][x1, x2]: position code of labels 'x1', 'x2' (simplex.py:
+                           58-59): p >= 0 row p (basic), -(j+1) column j, SMX_ABSENT none      */
+    int64_t npiv[2];    /* [parity]: pivot index of the step (history ring position)          */
+    int64_t reserved[4];
 } smx_ctl; /* 128 bytes */
 
 /* One per select workgroup (caller allocates nparts * sizeof(smx_part) bytes). */
@@ -97,9 +104,12 @@ int smx_tune_get(int32_t* variant, int32_t* blocks_per_cu, int32_t* nvariants,
                  int32_t* units_in_flight, int32_t* vec, int32_t* nt);
 
 /* Scan a freshly uploaded tableau into ctl slot `parity`; clears term, sets sel_status = IDLE,
- * and zeroes npivots when clear_count != 0. */
+ * zeroes npivots when clear_count != 0, and places labels x1/x2 at columns 0/1 (simplex.py:30). */
 int smx_reset(const double* T, const smx_shape* shape, int32_t parity, int32_t clear_count,
               smx_ctl* ctl, void* stream);
+
+/* Set the x1/x2 position codes of slot `parity` (after the host re-labelled a tableau). */
+int smx_set_xpos(smx_ctl* ctl, int32_t parity, int32_t x1code, int32_t x2code, void* stream);
 
 /* pick_element, part 1: per-workgroup partials of the selection for the tableau T. */
 int smx_select(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
@@ -110,20 +120,23 @@ int smx_finalize(const double* T, const smx_shape* shape, int32_t parity, smx_ct
                  const smx_part* parts, void* stream);
 
 /* recalculate_matrix: reduce the partials, record the outcome in ctl (sel_*, term, npivots,
- * log[npivots % log_cap] = (r, c)), and on SMX_PIVOT write the pivoted tableau to Tout.
- * Also primes ctl slot parity^1 for the next step (fused first-negative scans). */
+ * log[k % log_cap] = (r, c)), and on SMX_PIVOT write the pivoted tableau to Tout.  Also primes
+ * ctl slot parity^1 for the next step (fused first-negative scans) and, when xhist != NULL,
+ * records xhist[k % log_cap] = (x1, x2) of the new tableau (find_optimum, simplex.py:51-68;
+ * 0.0 for a non-basic label) -- the device-resident history of get_solution (:197-198). */
 int smx_update(const double* Tin, double* Tout, const smx_shape* shape, int32_t parity,
-               smx_ctl* ctl, const smx_part* parts, int32_t* log, int64_t log_cap,
+               smx_ctl* ctl, const smx_part* parts, int32_t* log, double* xhist, int64_t log_cap,
                void* stream);
 
 /* k pivots (select + update each), buffers buf0/buf1, first step's parity `parity`. */
 int smx_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
-            smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream);
+            smx_ctl* ctl, smx_part* parts, int32_t* log, double* xhist, int64_t log_cap,
+            void* stream);
 
 /* The same k-pivot chain captured as a hipGraph (opaque handle); replay with smx_graph_launch. */
 int smx_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
-                     int32_t k, smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap,
-                     void* stream, void** graph_out);
+                     int32_t k, smx_ctl* ctl, smx_part* parts, int32_t* log, double* xhist,
+                     int64_t log_cap, void* stream, void** graph_out);
 int smx_graph_launch(void* graph, void* stream);
 int smx_graph_destroy(void* graph);
 
@@ -131,8 +144,8 @@ int smx_graph_destroy(void* graph);
  * writes each update kernel's duration (ms) to host_update_ms[0..k-1] and the whole chain's
  * device time (first select start -> last update end) to *host_total_ms. */
 int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
-                  smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream,
-                  float* host_update_ms, float* host_total_ms);
+                  smx_ctl* ctl, smx_part* parts, int32_t* log, double* xhist, int64_t log_cap,
+                  void* stream, float* host_update_ms, float* host_total_ms);
 
 /* Forced-pivot microbenchmark of the update kernel alone: applies pivot (r, c) from Tin to Tout
  * without any selection (used to measure the kernel against the HBM roofline). */

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -26,6 +27,10 @@
 #pragma clang fp contract(off)
 
 static_assert(sizeof(smx_ctl) == 128, "smx_ctl layout");
+static_assert(offsetof(smx_ctl, term) == 16 && offsetof(smx_ctl, npivots) == 40 &&
+                  offsetof(smx_ctl, shard_off) == 56 && offsetof(smx_ctl, xpos) == 64 &&
+                  offsetof(smx_ctl, npiv) == 80,
+              "smx_ctl offsets (mirrored in simplex_mi355x/_lib.py)");
 static_assert(sizeof(smx_part) == 32, "smx_part layout");
 
 namespace {
@@ -235,11 +240,11 @@ __device__ void publish_shard_decision(const ShardDecision& d, const double* rec
     ctl->sel_r = d.r;
     ctl->sel_c = d.c;
     ctl->sel_owner = d.owner;
-    ctl->reserved[0] = d.off;
+    ctl->shard_off = d.off;
     ctl->sel_e = (d.status == SMX_PIVOT) ? recv[d.off + d.c] : 0.0;
     if (!commit) return;
     if (d.status == SMX_PIVOT) {
-        const int64_t k = ctl->npivots;
+        const int64_t k = ctl->npivots;   // sharded: only block 0 of the update reads/writes it
         if (log_cap > 0) {
             log[2 * (k % log_cap)] = d.r;
             log[2 * (k % log_cap) + 1] = d.c;
@@ -295,7 +300,24 @@ __global__ __launch_bounds__(1024) void k_reset(const double* __restrict__ T, in
         ctl->sel_r = SMX_NONE;
         ctl->sel_c = SMX_NONE;
         if (clear_count) ctl->npivots = 0;
+        ctl->npiv[parity] = ctl->npivots;
+        ctl->xpos[parity][0] = (m >= 1) ? -1 : SMX_ABSENT;   // 'x1' at column 0
+        ctl->xpos[parity][1] = (m >= 2) ? -2 : SMX_ABSENT;   // 'x2' at column 1
     }
+}
+
+__global__ void k_set_xpos(smx_ctl* __restrict__ ctl, int parity, int x1, int x2) {
+    if (threadIdx.x == 0) {
+        ctl->xpos[parity][0] = x1;
+        ctl->xpos[parity][1] = x2;
+    }
+}
+
+// Label movement of one pivot (simplex.py:152): the label at column c and the one at row r swap.
+__device__ __forceinline__ int move_label(int code, int r, int c) {
+    if (code == -(c + 1)) return r;
+    if (code == r) return -(c + 1);
+    return code;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -435,8 +457,9 @@ template <int MODE, int U, bool NTS, bool NTL, bool PIPE, bool DIAG = false>
 __global__ __launch_bounds__(kUpdBlock) void k_update(
     const double* __restrict__ Tin, double* __restrict__ Tout, int64_t ld, int rows_local,
     int n, int m, int flen, int fscan, int row0, int parity, smx_ctl* __restrict__ ctl,
-    const smx_part* __restrict__ parts, int nparts, int32_t* __restrict__ log, int64_t log_cap,
-    const double* __restrict__ recv, int forced_r, int forced_c) {
+    const smx_part* __restrict__ parts, int nparts, int32_t* __restrict__ log,
+    double* __restrict__ xhist, int64_t log_cap, const double* __restrict__ recv, int forced_r,
+    int forced_c) {
     __shared__ int s_dec[3];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -495,12 +518,20 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
                     ctl->sel_c = d.c;
                     if (d.status == SMX_PIVOT) {
                         ctl->sel_e = Tin[(int64_t)d.r * ld + d.c];
-                        const int64_t k = ctl->npivots;
+                        const int64_t k = ctl->npiv[parity];
                         if (log_cap > 0) {
                             log[2 * (k % log_cap)] = d.r;
                             log[2 * (k % log_cap) + 1] = d.c;
                         }
                         ctl->npivots = k + 1;
+                        ctl->npiv[parity ^ 1] = k + 1;
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            const int code = move_label(ctl->xpos[parity][q], d.r, d.c);
+                            ctl->xpos[parity ^ 1][q] = code;
+                            if (xhist && log_cap > 0 && code < 0)   // non-basic: value 0
+                                xhist[2 * (k % log_cap) + q] = 0.0;
+                        }
                     } else {
                         ctl->term = 1;
                     }
@@ -529,6 +560,14 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         prow = recv + s_off;
     }
     const double e = prow[c];
+    // history: rows whose new "-b" entry is x1 / x2 of the new tableau (find_optimum)
+    int hx0 = -1, hx1 = -1;
+    int64_t hslot = 0;
+    if (MODE == kSingle && xhist != nullptr && log_cap > 0) {
+        hx0 = move_label(ctl->xpos[parity][0], r, c);
+        hx1 = move_label(ctl->xpos[parity][1], r, c);
+        hslot = 2 * (ctl->npiv[parity] % log_cap);
+    }
     // local index of the pivot row, -1 when another rank owns it (never the f-row replica,
     // whose local index rows_local may equal r - row0 for a row of the next rank)
     const int r_local = (r >= row0 && r < row0 + rows_local) ? r - row0 : -1;
@@ -571,6 +610,10 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
                 else
                     o[h] = num / e;
                 if (MODE != kForced && jj < C) {
+                    if (MODE == kSingle && jj == m) {
+                        if (i == hx0) xhist[hslot] = o[h];
+                        if (i == hx1) xhist[hslot + 1] = o[h];
+                    }
                     if (i < rows_local) {
                         if (jj == m && o[h] < 0.0) lb = min(lb, row0 + i);
                     } else if (jj < fscan && o[h] < 0.0) {
@@ -732,7 +775,8 @@ int g_blocks_per_cu = 0;  // 0: kDefaultBpc, capped by the occupancy API (see bl
 constexpr int kDefaultBpc = 5;
 
 using UpdFn = void (*)(const double*, double*, int64_t, int, int, int, int, int, int, int,
-                       smx_ctl*, const smx_part*, int, int32_t*, int64_t, const double*, int, int);
+                       smx_ctl*, const smx_part*, int, int32_t*, double*, int64_t, const double*,
+                       int, int);
 
 template <int MODE>
 UpdFn upd_fn(int v) {
@@ -820,31 +864,32 @@ int update_grid(const smx_shape& s, int variant, const void* fn) {
 
 template <int MODE>
 int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int parity,
-                       smx_ctl* ctl, const smx_part* parts, int32_t* log, int64_t log_cap,
-                       const double* recv, int fr, int fc, hipStream_t st) {
+                       smx_ctl* ctl, const smx_part* parts, int32_t* log, double* xhist,
+                       int64_t log_cap, const double* recv, int fr, int fc, hipStream_t st) {
     const int v = g_variant;
     UpdFn fn = upd_fn<MODE>(v);
     hipLaunchKernelGGL(fn, dim3(update_grid(s, v, (const void*)fn)), dim3(kUpdBlock), 0, st, Tin,
                        Tout, s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl,
-                       parts, s.nparts, log, log_cap, recv, fr, fc);
+                       parts, s.nparts, log, xhist, log_cap, recv, fr, fc);
     return (int)hipGetLastError();
 }
 
 int launch_update(const double* Tin, double* Tout, const smx_shape& s, int parity, smx_ctl* ctl,
-                  const smx_part* parts, int32_t* log, int64_t log_cap, hipStream_t st) {
-    return launch_update_mode<kSingle>(Tin, Tout, s, parity, ctl, parts, log, log_cap, nullptr, 0,
-                                       0, st);
+                  const smx_part* parts, int32_t* log, double* xhist, int64_t log_cap,
+                  hipStream_t st) {
+    return launch_update_mode<kSingle>(Tin, Tout, s, parity, ctl, parts, log, xhist, log_cap,
+                                       nullptr, 0, 0, st);
 }
 
 int launch_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, smx_ctl* ctl,
-                 smx_part* parts, int32_t* log, int64_t log_cap, hipStream_t st) {
+                 smx_part* parts, int32_t* log, double* xhist, int64_t log_cap, hipStream_t st) {
     for (int step = 0; step < k; ++step) {
         const int p = (parity + step) & 1;
         double* tin = p ? buf1 : buf0;
         double* tout = p ? buf0 : buf1;
         int err = launch_select(tin, s, p, ctl, parts, st);
         if (err) return err;
-        err = launch_update(tin, tout, s, p, ctl, parts, log, log_cap, st);
+        err = launch_update(tin, tout, s, p, ctl, parts, log, xhist, log_cap, st);
         if (err) return err;
     }
     return 0;
@@ -918,21 +963,30 @@ int smx_finalize(const double* T, const smx_shape* shape, int32_t parity, smx_ct
 }
 
 int smx_update(const double* Tin, double* Tout, const smx_shape* shape, int32_t parity,
-               smx_ctl* ctl, const smx_part* parts, int32_t* log, int64_t log_cap,
+               smx_ctl* ctl, const smx_part* parts, int32_t* log, double* xhist, int64_t log_cap,
                void* stream) {
     if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
-    return launch_update(Tin, Tout, *shape, parity & 1, ctl, parts, log, log_cap, S(stream));
+    return launch_update(Tin, Tout, *shape, parity & 1, ctl, parts, log, xhist, log_cap,
+                         S(stream));
+}
+
+int smx_set_xpos(smx_ctl* ctl, int32_t parity, int32_t x1code, int32_t x2code, void* stream) {
+    hipLaunchKernelGGL(k_set_xpos, dim3(1), dim3(kWave), 0, S(stream), ctl, parity & 1, x1code,
+                       x2code);
+    return (int)hipGetLastError();
 }
 
 int smx_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
-            smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream) {
+            smx_ctl* ctl, smx_part* parts, int32_t* log, double* xhist, int64_t log_cap,
+            void* stream) {
     if (!shape_ok(shape) || buf0 == buf1 || k < 0) return (int)hipErrorInvalidValue;
-    return launch_chain(buf0, buf1, *shape, parity & 1, k, ctl, parts, log, log_cap, S(stream));
+    return launch_chain(buf0, buf1, *shape, parity & 1, k, ctl, parts, log, xhist, log_cap,
+                        S(stream));
 }
 
 int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
-                  smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap, void* stream,
-                  float* host_update_ms, float* host_total_ms) {
+                  smx_ctl* ctl, smx_part* parts, int32_t* log, double* xhist, int64_t log_cap,
+                  void* stream, float* host_update_ms, float* host_total_ms) {
     if (!shape_ok(shape) || buf0 == buf1 || k < 1 || !host_update_ms || !host_total_ms)
         return (int)hipErrorInvalidValue;
     hipStream_t st = S(stream);
@@ -954,7 +1008,7 @@ int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
         err = launch_select(tin, *shape, p, ctl, parts, st);
         if (err) break;
         (void)hipEventRecord(ev[2 * step], st);
-        err = launch_update(tin, tout, *shape, p, ctl, parts, log, log_cap, st);
+        err = launch_update(tin, tout, *shape, p, ctl, parts, log, xhist, log_cap, st);
         (void)hipEventRecord(ev[2 * step + 1], st);
     }
     if (!err) err = (int)hipEventSynchronize(ev[2 * k - 1]);
@@ -969,8 +1023,8 @@ int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
 }
 
 int smx_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
-                     int32_t k, smx_ctl* ctl, smx_part* parts, int32_t* log, int64_t log_cap,
-                     void* stream, void** graph_out) {
+                     int32_t k, smx_ctl* ctl, smx_part* parts, int32_t* log, double* xhist,
+                     int64_t log_cap, void* stream, void** graph_out) {
     if (!shape_ok(shape) || buf0 == buf1 || k < 1 || !graph_out) return (int)hipErrorInvalidValue;
     hipStream_t st = S(stream);
     Graph* g = new Graph();
@@ -979,7 +1033,8 @@ int smx_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t
         delete g;
         return (int)err;
     }
-    int lerr = launch_chain(buf0, buf1, *shape, parity & 1, k, ctl, parts, log, log_cap, st);
+    int lerr = launch_chain(buf0, buf1, *shape, parity & 1, k, ctl, parts, log, xhist, log_cap,
+                            st);
     err = hipStreamEndCapture(st, &g->graph);
     if (lerr || err != hipSuccess) {
         if (g->graph) (void)hipGraphDestroy(g->graph);
@@ -1014,8 +1069,8 @@ int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, i
                       int32_t c, void* stream) {
     if (!shape_ok(shape) || Tin == Tout) return (int)hipErrorInvalidValue;
     if (r < 0 || r >= shape->rows || c < 0 || c > shape->m) return (int)hipErrorInvalidValue;
-    return launch_update_mode<kForced>(Tin, Tout, *shape, 0, nullptr, nullptr, nullptr, 0,
-                                       nullptr, r, c, S(stream));
+    return launch_update_mode<kForced>(Tin, Tout, *shape, 0, nullptr, nullptr, nullptr, nullptr,
+                                       0, nullptr, r, c, S(stream));
 }
 
 int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
@@ -1045,8 +1100,8 @@ int smx_shard_update(const double* Tin, double* Tout, const double* recv, int32_
     if (!shape_ok(shape) || Tin == Tout || nranks < 1) return (int)hipErrorInvalidValue;
     smx_shape sh = *shape;
     sh.nparts = nranks;   // the update kernel's partial count is the rank count in shard mode
-    return launch_update_mode<kShard>(Tin, Tout, sh, parity & 1, ctl, nullptr, log, log_cap,
-                                      recv, 0, 0, S(stream));
+    return launch_update_mode<kShard>(Tin, Tout, sh, parity & 1, ctl, nullptr, log, nullptr,
+                                      log_cap, recv, 0, 0, S(stream));
 }
 
 int smx_shard_begin(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,

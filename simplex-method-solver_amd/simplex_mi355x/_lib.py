@@ -25,8 +25,10 @@ PART_BYTES = 32
 CTL_DTYPE = np.dtype([
     ("negb", "<i4", (2,)), ("negf", "<i4", (2,)), ("term", "<i4"), ("sel_status", "<i4"),
     ("sel_r", "<i4"), ("sel_c", "<i4"), ("sel_e", "<f8"), ("npivots", "<i8"),
-    ("sel_owner", "<i4"), ("pad0", "<i4"), ("reserved", "<i8", (9,)),
+    ("sel_owner", "<i4"), ("pad0", "<i4"), ("shard_off", "<i8"), ("xpos", "<i4", (2, 2)),
+    ("npiv", "<i8", (2,)), ("reserved", "<i8", (4,)),
 ])
+ABSENT = -0x80000000
 assert CTL_DTYPE.itemsize == CTL_BYTES
 
 
@@ -40,7 +42,7 @@ class Shape(ctypes.Structure):
 _lib = None
 
 EXPORTS = (
-    "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_reset", "smx_select", "smx_finalize", "smx_update",
+    "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_set_xpos", "smx_reset", "smx_select", "smx_finalize", "smx_update",
     "smx_run", "smx_run_timed", "smx_graph_create", "smx_graph_launch", "smx_graph_destroy", "smx_update_forced",
     "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
     "smx_shard_finish",
@@ -69,12 +71,13 @@ def load():
         "smx_reset": ([vp, sp, i32, i32, vp, vp], ctypes.c_int),
         "smx_select": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),
         "smx_finalize": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),
-        "smx_update": ([vp, vp, sp, i32, vp, vp, vp, i64, vp], ctypes.c_int),
-        "smx_run": ([vp, vp, sp, i32, i32, vp, vp, vp, i64, vp], ctypes.c_int),
-        "smx_run_timed": ([vp, vp, sp, i32, i32, vp, vp, vp, i64, vp,
+        "smx_update": ([vp, vp, sp, i32, vp, vp, vp, vp, i64, vp], ctypes.c_int),
+        "smx_set_xpos": ([vp, i32, i32, i32, vp], ctypes.c_int),
+        "smx_run": ([vp, vp, sp, i32, i32, vp, vp, vp, vp, i64, vp], ctypes.c_int),
+        "smx_run_timed": ([vp, vp, sp, i32, i32, vp, vp, vp, vp, i64, vp,
                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)],
                           ctypes.c_int),
-        "smx_graph_create": ([vp, vp, sp, i32, i32, vp, vp, vp, i64, vp,
+        "smx_graph_create": ([vp, vp, sp, i32, i32, vp, vp, vp, vp, i64, vp,
                               ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "smx_graph_launch": ([vp, vp], ctypes.c_int),
         "smx_graph_destroy": ([vp], ctypes.c_int),

@@ -9,6 +9,8 @@ Layout in HBM (one object per tableau, owned by torch tensors):
 * ``ctl``   : 128-B ``struct smx_ctl`` (first-negative slots, selection, pivot counter).
 * ``parts`` : ``nparts`` x 32-B ``struct smx_part`` select partials.
 * ``log``   : ``int32[log_cap][2]`` ring of applied pivots ``(r, c)``, drained by the host.
+* ``xhist`` : ``float64[log_cap][2]`` ring of ``(x1, x2)`` of the tableau after each pivot
+  (find_optimum, simplex.py:51-68), written by the update kernel itself.
 
 All launches go to one dedicated HIP stream per tableau; the host synchronises only when it
 reads the control block.
@@ -69,6 +71,7 @@ class DeviceTableau:
             self.parts = torch.zeros(self.nparts * _lib.PART_BYTES // 8, dtype=torch.int64,
                                      device=self.device)
             self.log = torch.zeros(2 * log_cap, dtype=torch.int32, device=self.device)
+            self.xhist = torch.zeros(2 * log_cap, dtype=torch.float64, device=self.device)
         self.log_cap = log_cap
         self.step = 0
         self._pending = False   # chained pivots enqueued whose outcome the host has not read
@@ -118,14 +121,28 @@ class DeviceTableau:
 
     def read_log(self, start: int, stop: int) -> np.ndarray:
         """Pivots start..stop-1 (absolute counts) from the device ring."""
+        return self._ring(self.log, start, stop, np.int32)
+
+    def read_xhist(self, start: int, stop: int) -> np.ndarray:
+        """(x1, x2) after pivots start..stop-1 (absolute counts) from the device ring."""
+        return self._ring(self.xhist, start, stop, np.float64)
+
+    def _ring(self, buf, start, stop, dtype):
         if stop <= start:
-            return np.zeros((0, 2), dtype=np.int32)
+            return np.zeros((0, 2), dtype=dtype)
         if stop - start > self.log_cap:
             raise RuntimeError("pivot log overrun: drain the log more often")
-        with torch.cuda.stream(self.stream):
-            ring = self.log.cpu().numpy().reshape(-1, 2)
         pos = np.arange(start, stop) % self.log_cap
-        return ring[pos]
+        lo, hi = int(pos.min()), int(pos.max()) + 1
+        with torch.cuda.stream(self.stream):
+            ring = buf.view(-1, 2)[lo:hi].cpu().numpy()
+        return ring[pos - lo]
+
+    def set_label_positions(self, x1code: int, x2code: int) -> None:
+        """Tell the device where labels x1/x2 sit (after a host-side re-labelling)."""
+        with torch.cuda.stream(self.stream):
+            _lib.check(_lib.load().smx_set_xpos(self.ctl.data_ptr(), self.step & 1, x1code,
+                                                x2code, self.stream.cuda_stream), "smx_set_xpos")
 
     # -- pivot loop -----------------------------------------------------------------------
     def select(self) -> None:
@@ -149,7 +166,8 @@ class DeviceTableau:
         self.settle()
         p = self.step & 1
         with torch.cuda.stream(self.stream):
-            ops.update(self.buf[p], self.buf[p ^ 1], self.ctl, self.parts, self.log, self.shape, p)
+            ops.update(self.buf[p], self.buf[p ^ 1], self.ctl, self.parts, self.log, self.xhist,
+                       self.shape, p)
         self.step += 1
 
     def run(self, k: int, graph: bool = True) -> None:
@@ -167,7 +185,7 @@ class DeviceTableau:
                     g = self._make_graph(p, k)
                 g.launch(self.stream.cuda_stream)
             else:
-                ops.run(self.buf, self.ctl, self.parts, self.log, self.shape, p, k)
+                ops.run(self.buf, self.ctl, self.parts, self.log, self.xhist, self.shape, p, k)
         # optimistic: if the chain stops early every later kernel is a no-op, and sync_state()
         # replaces this with the device's exact count
         self.step += k
@@ -186,8 +204,9 @@ class DeviceTableau:
         sh = ops.make_shape(self.shape)
         _lib.check(_lib.load().smx_run_timed(
             self.buf[0].data_ptr(), self.buf[1].data_ptr(), ctypes.byref(sh), p, k,
-            self.ctl.data_ptr(), self.parts.data_ptr(), self.log.data_ptr(), self.log_cap,
-            self.stream.cuda_stream, upd, ctypes.byref(tot)), "smx_run_timed")
+            self.ctl.data_ptr(), self.parts.data_ptr(), self.log.data_ptr(),
+            self.xhist.data_ptr(), self.log_cap, self.stream.cuda_stream, upd,
+            ctypes.byref(tot)), "smx_run_timed")
         self.step += k
         self._pending = True
         return np.frombuffer(upd, dtype=np.float32).copy(), float(tot.value)
@@ -213,7 +232,8 @@ class DeviceTableau:
         b0, b1 = self.buf[0].data_ptr(), self.buf[1].data_ptr()
         _lib.check(_lib.load().smx_graph_create(
             b0, b1, ctypes.byref(sh), parity, k, self.ctl.data_ptr(), self.parts.data_ptr(),
-            self.log.data_ptr(), self.log_cap, self.stream.cuda_stream, ctypes.byref(h)),
+            self.log.data_ptr(), self.xhist.data_ptr(), self.log_cap, self.stream.cuda_stream,
+            ctypes.byref(h)),
             "smx_graph_create")
         g = Graph(h.value)
         self._graphs[(parity, k)] = g

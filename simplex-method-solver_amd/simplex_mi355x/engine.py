@@ -56,6 +56,84 @@ class Info:
         self.optimum = optimum
 
 
+class LazyInfo(Info):
+    """An ``Info`` whose ``table`` is materialised on first access from the device history
+    (checkpoint + replay of the logged pivots with the bit-identical update kernel), so a
+    get_solution history of a large tableau costs O(pivots) host memory, not O(pivots x R x C)."""
+
+    def __init__(self, row, column, history, step, i, j, x1, x2, optimum, table=None):
+        self.row = row.copy()
+        self.column = column.copy()
+        self._history = history
+        self._step = step
+        self._table = table
+        self.i = i
+        self.j = j
+        self.x1 = x1
+        self.x2 = x2
+        self.optimum = optimum
+
+    @property
+    def table(self):
+        if self._table is None:
+            self._table = self._history.table(self._step)
+        return self._table
+
+    @table.setter
+    def table(self, value):
+        self._table = value
+
+
+class History:
+    """Device checkpoints of the tableau every ``every`` pivots (within ``budget_bytes``) plus
+    the host copy of the pivot log; ``table(step)`` replays from the nearest checkpoint."""
+
+    def __init__(self, solver, every=256, budget_bytes=8 << 30):
+        import torch
+        self.sm = solver
+        self.dev = solver._dev
+        self.every = max(1, int(every))
+        self.budget = budget_bytes
+        self.ckpt = {}
+        self.base = solver.pivots          # pivot count at the start of this history
+        self._torch = torch
+        self._scratch = None
+        self.checkpoint(self.base)
+
+    def _bytes(self):
+        return sum(t.numel() * 8 for t in self.ckpt.values())
+
+    def checkpoint(self, step):
+        dev = self.dev
+        if step in self.ckpt or (step - self.base) % self.every and step != self.base:
+            return
+        one = (dev.rows + 1) * dev.ld * 8
+        if self.ckpt and self._bytes() + one > self.budget:
+            return
+        with self._torch.cuda.stream(dev.stream):
+            self.ckpt[step] = dev.cur().clone()
+
+    def table(self, step):
+        dev, torch = self.dev, self._torch
+        s0 = max(k for k in self.ckpt if k <= step)
+        log = self.sm.pivot_log
+        with torch.cuda.stream(dev.stream):
+            if self._scratch is None:
+                self._scratch = torch.empty((2, dev.rows + 1, dev.ld), dtype=torch.float64,
+                                            device=dev.device)
+            sc = self._scratch
+            sc[0].copy_(self.ckpt[s0])
+            from . import ops
+            for t in range(s0, step):
+                a = (t - s0) & 1
+                r, c = log[t]
+                ops.update_forced(sc[a], sc[a ^ 1], dev.shape, r, c)
+            T = sc[(step - s0) & 1][:, :dev.C].cpu().numpy()
+        rows = T[:self.sm.n].tolist()
+        rows.append(T[self.sm.n, :min(self.sm.flen, self.sm.m + 1)].tolist())
+        return rows
+
+
 def _dense_from_lists(constraints, function, m):
     n = len(constraints)
     T = np.zeros((n + 1, m + 1), dtype=np.float64)
@@ -204,10 +282,18 @@ class SimplexMethod:
             return True
         return False
 
-    def get_solution(self, max_pivots=None, detect_cycles=False):
+    LAZY_ELEMENTS = 1 << 20   # above this many tableau entries get_solution snapshots lazily
+
+    def get_solution(self, max_pivots=None, detect_cycles=False, lazy=None, chunk=256):
         """simplex.py:179-199.  Opt-in additions (defaults = the reference's behaviour):
         ``max_pivots`` bounds the loop (the list ends, ``status == 'cap'``); ``detect_cycles``
-        ends it when the basis repeats (``status == 'cycle'``, ``self.cycle``)."""
+        ends it when the basis repeats (``status == 'cycle'``, ``self.cycle``).  ``lazy``
+        (default: automatic above ``LAZY_ELEMENTS`` entries) runs the chained device loop and
+        returns ``LazyInfo`` snapshots whose tables are materialised on access."""
+        if lazy is None:
+            lazy = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS
+        if lazy and self.flen in (self.m, self.m + 1) and self.flen >= 2:
+            return self._get_solution_lazy(max_pivots, detect_cycles, chunk)
         result = []
         result.append(Info(self.row, self.column, self.table, None, None, 0, 0, 0))
         done = 0
@@ -234,6 +320,55 @@ class SimplexMethod:
             if self._track(i, j, detect_cycles):
                 self.status = "cycle"
                 break
+        return result
+
+    def _get_solution_lazy(self, max_pivots, detect_cycles, chunk):
+        """get_solution's loop (simplex.py:184-198) chained on the device; the (i, j) of every
+        step and its (x1, x2) come from the device rings, tables from History on demand."""
+        hist = History(self, every=chunk)
+        first = LazyInfo(self.row, self.column, hist, self.pivots, None, None, 0, 0, 0,
+                         table=copy.deepcopy(self.table) if self._pristine else None)
+        result = [first]
+        dev = self._dev
+        budget = float("inf") if max_pivots is None else int(max_pivots)
+        start = self.pivots
+        status = None
+        while self.pivots - start < budget:
+            k = int(min(chunk, budget - (self.pivots - start), dev.log_cap))
+            before = dev.step
+            dev.run(k, graph=(k == chunk))
+            ctl = dev.sync_state()
+            done = int(ctl["npivots"])
+            logs = dev.read_log(before, done)
+            xs = dev.read_xhist(before, done)
+            cycled = False
+            for (r, c), (v1, v2) in zip(logs, xs):
+                r, c = int(r), int(c)
+                result[-1].i, result[-1].j = r, c
+                self.row[c], self.column[r] = self.column[r], self.row[c]   # simplex.py:152
+                self.pivot_log.append((r, c))
+                self._pristine = False
+                x1 = float(v1) if 'x1' in self.column else 0                # simplex.py:51-68
+                x2 = float(v2) if 'x2' in self.column else 0
+                result.append(LazyInfo(self.row, self.column, hist, self.pivots, None, None,
+                                       x1, x2, self.f(x1, x2)))
+                cycled = self._track(r, c, detect_cycles) or cycled   # stop after this chunk
+            hist.checkpoint(self.pivots)
+            if cycled:
+                status = "cycle"
+                break
+            if ctl["term"]:
+                status = int(ctl["sel_status"])
+                break
+        if status is None:
+            self.status = "cap"
+        elif status == "cycle":
+            self.status = "cycle"
+        elif status == _lib.OPTIMUM:
+            self.status = "optimum"
+        elif status in MESSAGES:
+            self.status = "error"
+            result.append(Error(MESSAGES[status]))
         return result
 
     # ---------------------------------------------------------------- additions ----------

@@ -93,35 +93,44 @@ def finalize(T: Tensor, ctl: Tensor, parts: Tensor, shape: list[int], parity: in
                                         _ptr(parts), _stream()), "smx_finalize")
 
 
-@torch.library.custom_op("smx::update", mutates_args=("tout", "ctl", "log"))
-def update(tin: Tensor, tout: Tensor, ctl: Tensor, parts: Tensor, log: Tensor,
+def _xhist_ok(xhist: Tensor, log: Tensor) -> None:
+    if xhist.dtype != torch.float64 or not xhist.is_cuda or not xhist.is_contiguous() or \
+            xhist.numel() < log.numel():
+        raise ValueError("xhist: expected a contiguous float64 CUDA tensor as long as log")
+
+
+@torch.library.custom_op("smx::update", mutates_args=("tout", "ctl", "log", "xhist"))
+def update(tin: Tensor, tout: Tensor, ctl: Tensor, parts: Tensor, log: Tensor, xhist: Tensor,
            shape: list[int], parity: int) -> None:
-    """recalculate_matrix (simplex.py:143-177) from tin into tout."""
+    """recalculate_matrix (simplex.py:143-177) from tin into tout; logs (r, c) and the new
+    tableau's (x1, x2) (find_optimum, simplex.py:51-68) into the history rings."""
     _table_ok(tin, shape, "tin")
     _table_ok(tout, shape, "tout")
     if tin.data_ptr() == tout.data_ptr():
         raise ValueError("update is out of place: tin and tout must differ")
     _bytes_ok(ctl, _lib.CTL_BYTES, "ctl")
     _parts_ok(parts, shape)
+    _xhist_ok(xhist, log)
     sh = make_shape(shape)
     _lib.check(_lib.load().smx_update(_ptr(tin), _ptr(tout), ctypes.byref(sh), parity, _ptr(ctl),
-                                      _ptr(parts), _ptr(log), _log_cap(log), _stream()),
-               "smx_update")
+                                      _ptr(parts), _ptr(log), _ptr(xhist), _log_cap(log),
+                                      _stream()), "smx_update")
 
 
-@torch.library.custom_op("smx::run", mutates_args=("buf", "ctl", "parts", "log"))
-def run(buf: Tensor, ctl: Tensor, parts: Tensor, log: Tensor, shape: list[int], parity: int,
-        k: int) -> None:
+@torch.library.custom_op("smx::run", mutates_args=("buf", "ctl", "parts", "log", "xhist"))
+def run(buf: Tensor, ctl: Tensor, parts: Tensor, log: Tensor, xhist: Tensor, shape: list[int],
+        parity: int, k: int) -> None:
     """k chained pivots (the loop of get_solution, simplex.py:184-198) on buf[0]/buf[1]."""
     if buf.dim() != 3 or buf.shape[0] != 2:
         raise ValueError("buf must be (2, R, ld)")
     _table_ok(buf[0], shape, "buf[0]")
     _bytes_ok(ctl, _lib.CTL_BYTES, "ctl")
     _parts_ok(parts, shape)
+    _xhist_ok(xhist, log)
     sh = make_shape(shape)
     _lib.check(_lib.load().smx_run(_ptr(buf[0]), _ptr(buf[1]), ctypes.byref(sh), parity, k,
-                                   _ptr(ctl), _ptr(parts), _ptr(log), _log_cap(log), _stream()),
-               "smx_run")
+                                   _ptr(ctl), _ptr(parts), _ptr(log), _ptr(xhist),
+                                   _log_cap(log), _stream()), "smx_run")
 
 
 @torch.library.custom_op("smx::update_forced", mutates_args=("tout",))

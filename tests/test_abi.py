@@ -43,10 +43,10 @@ def test_struct_layouts_match_header():
     from simplex_mi355x import _lib
     assert ctypes.sizeof(_lib.Shape) == 32
     assert _lib.CTL_DTYPE.itemsize == 128
-    # offsets used by the host: term at byte 16, npivots at 40, reserved at 56
-    assert _lib.CTL_DTYPE.fields["term"][1] == 16
-    assert _lib.CTL_DTYPE.fields["npivots"][1] == 40
-    assert _lib.CTL_DTYPE.fields["reserved"][1] == 56
+    # offsets used by the host and the kernels (include/smx.h)
+    f = _lib.CTL_DTYPE.fields
+    assert (f["term"][1], f["npivots"][1], f["shard_off"][1], f["xpos"][1], f["npiv"][1]) == \
+        (16, 40, 56, 64, 80)
 
 
 def test_host_helpers_without_gpu():

@@ -249,3 +249,58 @@ def test_bench_single_and_sharded_paths():
                            "--no-cpu-baseline"] + extra)
         assert rec["trajectory_valid"] and rec["n_gpus"] == 1 and rec["value"] > 0
         assert rec["roofline"]["bound"] == "hbm" and 0 < rec["roofline"]["frac"] < 1
+
+
+# ----------------------------------------------------------------------------------------------
+# 8. device-resident history: lazy get_solution == eager get_solution, tables bit-identical
+def _same_infos(a, b):
+    import simplex
+    assert len(a) == len(b)
+    for x, y in zip(a, b):
+        if isinstance(y, simplex.Error):
+            assert isinstance(x, simplex.Error) and str(x) == str(y)
+            continue
+        assert (x.row, x.column, x.i, x.j) == (y.row, y.column, y.i, y.j)
+        assert same_value(x.x1, y.x1) and same_value(x.x2, y.x2)
+        assert same_value(x.optimum, y.optimum)
+        assert same_table(x.table, y.table)
+
+
+@pytest.mark.parametrize("k", range(0, 40, 3))
+def test_lazy_history_matches_eager_on_fixtures(k):
+    import simplex
+    rec = load("random.json")[k]
+    if rec["outcome"]["kind"] == "cap":
+        pytest.skip("cycling fixture")
+    cons, func = dec_input(rec["input"])
+    eager = simplex.SimplexMethod([list(r) for r in cons], list(func)).get_solution(lazy=False)
+    lazy = simplex.SimplexMethod([list(r) for r in cons], list(func)).get_solution(lazy=True,
+                                                                                 chunk=7)
+    _same_infos(lazy, eager)
+    assert [table_hash(i.table) for i in lazy if isinstance(i, simplex.Info)] == \
+        [s["hash"] for s in rec["steps"]]
+
+
+def test_lazy_history_large_tableau_vs_oracle():
+    """1200 x 1100 tableau, 90 pivots: automatic lazy mode; tables of chosen steps replayed on the
+    device equal the C oracle's tables at those steps bit for bit; x1/x2 per step as well."""
+    import simplex
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    n, m, k = 1199, 1099, 90
+    T = lp.dense_tableau("uniform", 4, n, m)
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    out = sm.get_solution(max_pivots=k, chunk=32)
+    assert sm.status == "cap" and len(out) == k + 1
+    for step in (0, 1, 31, 32, 33, 64, 90):
+        Tref, st, done, log = c_oracle.run(T, n, m, m, step, threads=8)
+        got = np.array(out[step].table[:n])
+        assert np.array_equal(got.view(np.int64), Tref[:n].view(np.int64)), step
+        assert [tuple(map(int, x)) for x in log] == sm.pivot_log[:step]
+    # x1 / x2 per step: the reference's find_optimum on the materialised table
+    for step in (5, 47, 90):
+        info = out[step]
+        tab = info.table
+        for name, val in (("x1", info.x1), ("x2", info.x2)):
+            exp = tab[info.column.index(name)][-1] if name in info.column else 0
+            assert same_value(val, exp)
