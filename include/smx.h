@@ -152,6 +152,17 @@ int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
 int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, int32_t r,
                       int32_t c, void* stream);
 
+/* ---- batched small LPs (one wavefront per LP; the UI's workload) --------------------------
+ * B problems, each packed as rows 0..n_b (f-row = row n_b) of a Rmax x ldb fp64 block (Rmax <=
+ * 64, ldb <= 64, ldb >= m_b + 1); dims = int32 [B][3] = (n, m, len(function)).  Runs the whole
+ * get_solution loop (simplex.py:184-198) per problem, at most max_pivots pivots.  Outputs per
+ * problem: final table (out, same layout), status (SMX_* ; SMX_PIVOT = cap reached), pivot count,
+ * rc = int32 [B][max_pivots][2], xv = fp64 [B][max_pivots][2] (x1, x2 after each pivot), and when
+ * snaps != NULL the table after each pivot, fp64 [B][max_pivots][Rmax][ldb]. */
+int smx_batch_solve(const double* tabs, const int32_t* dims, int32_t B, int32_t Rmax,
+                    int32_t ldb, int32_t max_pivots, double* out, int32_t* rc, double* xv,
+                    double* snaps, int32_t* status, int32_t* npivots, void* stream);
+
 /* ---- row-sharded engine (one process per GPU; exchange = caller's all-gather) ----------
  * Local tableau: shape->rows constraint rows (global rows row0 .. row0+rows-1) + a replica
  * of the f-row as local row `rows`.  Per pivot:

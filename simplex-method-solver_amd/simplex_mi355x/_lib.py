@@ -44,7 +44,7 @@ _lib = None
 EXPORTS = (
     "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_set_xpos", "smx_reset", "smx_select", "smx_finalize", "smx_update",
     "smx_run", "smx_run_timed", "smx_graph_create", "smx_graph_launch", "smx_graph_destroy", "smx_update_forced",
-    "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
+    "smx_batch_solve", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
     "smx_shard_finish",
 )
 
@@ -85,6 +85,8 @@ def load():
         "smx_shard_pack": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_merge": ([vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_shard_update": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
+        "smx_batch_solve": ([vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp],
+                            ctypes.c_int),
         "smx_shard_begin": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp, vp, vp], ctypes.c_int),
     }
