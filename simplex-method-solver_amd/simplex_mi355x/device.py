@@ -50,13 +50,13 @@ class DeviceTableau:
 
     def __init__(self, dense: np.ndarray, n: int, m: int, flen: int, *, device=None,
                  row0: int = 0, n_global: int | None = None, log_cap: int = 1 << 16,
-                 pad_to: int = 16, ld_extra: int = 0):
+                 pad_to: int = 16, ld_extra: int = 0, defer_upload: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("simplex_mi355x needs an MI355X (HIP device); there is no CPU path")
         _lib.load()
         rows = dense.shape[0] - 1
         C = m + 1
-        if dense.shape[1] < C:
+        if dense.shape[1] < C and not defer_upload:
             raise ValueError("dense tableau narrower than m + 1")
         self.device = torch.device(device if device is not None else "cuda")
         self.rows, self.n, self.m, self.flen, self.row0 = rows, (n if n_global is None else n_global), m, flen, row0
@@ -77,7 +77,8 @@ class DeviceTableau:
         self._pending = False   # chained pivots enqueued whose outcome the host has not read
         self._term = False      # a terminal outcome may be latched in ctl.term
         self._graphs: dict[tuple[int, int], Graph] = {}
-        self.upload(dense)
+        if not defer_upload:
+            self.upload(dense)
 
     # -- data movement --------------------------------------------------------------------
     def upload(self, dense: np.ndarray) -> None:
@@ -86,6 +87,14 @@ class DeviceTableau:
         with torch.cuda.stream(self.stream):
             self.buf.zero_()
             self.buf[0, :, :self.C].copy_(host)
+            self.step = 0
+            ops.reset(self.buf[0], self.ctl, self.shape, 0, 1)
+        self._pending = False
+        self._term = False
+
+    def reset_state(self) -> None:
+        """Prime the control block for whatever buf[0] now holds (pivot count = 0)."""
+        with torch.cuda.stream(self.stream):
             self.step = 0
             ops.reset(self.buf[0], self.ctl, self.shape, 0, 1)
         self._pending = False

@@ -113,6 +113,16 @@ class History:
         with self._torch.cuda.stream(dev.stream):
             self.ckpt[step] = dev.cur().clone()
 
+    def checkpoint_now(self):
+        """Checkpoint the current device table regardless of spacing (budget permitting)."""
+        dev = self.dev
+        step = self.sm.pivots
+        one = (dev.rows + 1) * dev.ld * 8
+        if step in self.ckpt or (self.ckpt and self._bytes() + one > self.budget):
+            return
+        with self._torch.cuda.stream(dev.stream):
+            self.ckpt[step] = dev.cur().clone()
+
     def table(self, step):
         dev, torch = self.dev, self._torch
         s0 = max(k for k in self.ckpt if k <= step)
@@ -172,6 +182,35 @@ class SimplexMethod:
         self.status = "ready"
         self.cycle = None          # (first step of a repeated basis, period) when detected
         self._tracker = None
+
+    @classmethod
+    def from_file(cls, path, device=None):
+        """Load a problem file: the reference UI's ``.txt`` (main.py:402-495; objective =
+        gradient[:-1], main.py:312) or a binary ``.smx`` tableau streamed straight into HBM."""
+        from . import problem_io
+        if path.endswith(".smx"):
+            dev = problem_io.load_device(path, device=device)
+            return cls._from_device(dev)
+        return cls(*problem_io.solver_inputs_txt(path), device=device)
+
+    @classmethod
+    def _from_device(cls, dev):
+        """A SimplexMethod around an already-resident tableau (no host lists of the table)."""
+        self = cls.__new__(cls)
+        self.n, self.m, self.flen = dev.rows, dev.m, dev.flen
+        self.invalid_index = 1 + max(self.n, self.m)
+        with __import__("torch").cuda.stream(dev.stream):
+            self.function = dev.buf[0, self.n, :min(dev.flen, dev.C)].cpu().tolist()
+        self.row = ['x' + str(_) for _ in range(1, self.m + 1)] + ['-b']
+        self.column = ['y' + str(_) for _ in range(1, self.n + 1)] + ['f']
+        self._initial = None
+        self._dev = dev
+        self._pristine = False
+        self.pivot_log = []
+        self.status = "ready"
+        self.cycle = None
+        self._tracker = None
+        return self
 
     # ---------------------------------------------------------------- state views --------
     @property
@@ -389,7 +428,12 @@ class SimplexMethod:
             return self.get_solution(max_pivots=max_pivots, detect_cycles=detect_cycles)
         if self.flen not in (self.m, self.m + 1) or self.flen < 2:
             return self._solve_stepwise(max_pivots, detect_cycles)
-        first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
+        big = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS
+        hist = History(self, every=1 << 62) if big else None    # one checkpoint: the start
+        if big:
+            first = LazyInfo(self.row, self.column, hist, self.pivots, None, None, 0, 0, 0)
+        else:
+            first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
         start = self.pivots
         budget = float("inf") if max_pivots is None else int(max_pivots)
         dev = self._dev
@@ -418,7 +462,13 @@ class SimplexMethod:
         if self.pivots > start:
             first.i, first.j = self.pivot_log[start]
         x1, x2 = self.find_optimum()
-        out.append(Info(self.row, self.column, self.table, None, None, x1, x2, self.f(x1, x2)))
+        if big:   # the final table is the current device table: materialise it on access
+            hist.checkpoint_now()
+            out.append(LazyInfo(self.row, self.column, hist, self.pivots, None, None, x1, x2,
+                                self.f(x1, x2)))
+        else:
+            out.append(Info(self.row, self.column, self.table, None, None, x1, x2,
+                            self.f(x1, x2)))
         if status is None:
             self.status = "cap"
         elif status == "cycle":

@@ -304,3 +304,33 @@ def test_lazy_history_large_tableau_vs_oracle():
         for name, val in (("x1", info.x1), ("x2", info.x2)):
             exp = tab[info.column.index(name)][-1] if name in info.column else 0
             assert same_value(val, exp)
+
+
+# ----------------------------------------------------------------------------------------------
+# 9. problem files: .txt (the reference UI's format) and .smx streamed into HBM
+def test_from_file_txt_and_smx(tmp_path):
+    import simplex
+    from simplex_mi355x import lp, problem_io
+    case = load("examples.json")["ex1"]
+    cons, func = dec_input(case["input"])
+    p = str(tmp_path / "ex1.txt")
+    problem_io.save_txt(p, cons, list(func) + [0.0], 5)
+    got = simplex.SimplexMethod.from_file(p).get_solution()
+    exp = simplex.SimplexMethod([list(map(float, r)) for r in cons],
+                                list(map(float, func))).get_solution()
+    assert [(g.i, g.j) for g in got] == [(e.i, e.j) for e in exp]
+    assert same_table(got[-1].table, exp[-1].table)
+    n = m = 1500
+    T = lp.dense_tableau("uniform", 6, n, m)
+    q = str(tmp_path / "big.smx")
+    problem_io.save_smx(q, T, n, m, m)
+    a = simplex.SimplexMethod.from_file(q)
+    b = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    ra = a.solve(record_history=False, max_pivots=60, chunk=30)
+    rb = b.solve(record_history=False, max_pivots=60, chunk=30)
+    assert a.pivot_log == b.pivot_log
+    assert np.array_equal(np.array(ra[-1].table[:n]).view(np.int64),
+                          np.array(rb[-1].table[:n]).view(np.int64))
+    assert np.array_equal(np.array(ra[-1].table[n]).view(np.int64),
+                          np.array(rb[-1].table[n]).view(np.int64))
+    assert np.array_equal(np.array(ra[0].table[:n]).view(np.int64), T[:n].view(np.int64))
