@@ -192,6 +192,21 @@ int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_
                      const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
                      int64_t log_cap, void* ev_before, void* ev_after, void* stream);
 
+/* Native RCCL driver (one communicator per rank; the unique id is created on rank 0 and
+ * shipped to the others by any bootstrap, e.g. torch.distributed.broadcast_object_list).
+ * smx_shard_run = k x {select, pack, ncclAllGather on `stream`, update}: no cross-stream waits,
+ * no host synchronisation.  RCCL failures are returned as -1000 - ncclResult_t. */
+int smx_comm_unique_id(void* id_out /* 128 bytes */);
+int smx_comm_init(void** comm_out, int32_t nranks, const void* id, int32_t rank);
+int smx_comm_destroy(void* comm);
+int smx_shard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                  smx_ctl* ctl, smx_part* parts, double* send, double* recv, int32_t nranks,
+                  void* comm, int32_t* log, int64_t log_cap, void* stream);
+int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                        int32_t k, smx_ctl* ctl, smx_part* parts, double* send, double* recv,
+                        int32_t nranks, void* comm, int32_t* log, int64_t log_cap, void* stream,
+                        float* host_update_ms, float* host_total_ms);
+
 #ifdef __cplusplus
 }
 #endif

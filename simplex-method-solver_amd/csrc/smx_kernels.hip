@@ -22,6 +22,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <rccl/rccl.h>
+
 #include "smx.h"
 
 #pragma clang fp contract(off)
@@ -1264,6 +1266,103 @@ int smx_batch_solve(const double* tabs, const int32_t* dims, int32_t B, int32_t 
         hipLaunchKernelGGL(k_batch<64>, grid, block, 0, st, tabs, dims, B, Rmax, ldb, max_pivots,
                            out, rc, xv, snaps, status, npivots);
     return (int)hipGetLastError();
+}
+
+
+// ---- native RCCL shard driver: the all-gather on the solver's own stream --------------------
+// (torch.distributed would run it on its own NCCL stream: one cross-stream event wait per pivot,
+// ~14 us measured; here the whole pivot -- select, pack, ncclAllGather, update -- is one
+// stream-ordered sequence that can also be captured in a hipGraph.)
+static int nccl_err(ncclResult_t r) { return r == ncclSuccess ? 0 : -1000 - (int)r; }
+
+int smx_comm_unique_id(void* id_out) {
+    if (!id_out) return (int)hipErrorInvalidValue;
+    ncclUniqueId id;
+    const int err = nccl_err(ncclGetUniqueId(&id));
+    if (!err) memcpy(id_out, &id, sizeof(id));
+    return err;
+}
+
+int smx_comm_init(void** comm_out, int32_t nranks, const void* id, int32_t rank) {
+    if (!comm_out || !id || nranks < 1 || rank < 0 || rank >= nranks)
+        return (int)hipErrorInvalidValue;
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    const int err = nccl_err(ncclCommInitRank(&comm, nranks, uid, rank));
+    if (!err) *comm_out = comm;
+    return err;
+}
+
+int smx_comm_destroy(void* comm) {
+    if (!comm) return 0;
+    return nccl_err(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+}
+
+namespace {
+int shard_pivot(double* tin, double* tout, const smx_shape& s, int p, smx_ctl* ctl,
+                smx_part* parts, double* send, double* recv, int nranks, ncclComm_t comm,
+                int32_t* log, int64_t log_cap, hipEvent_t e0, hipEvent_t e1, hipStream_t st) {
+    int err = launch_select(tin, s, p, ctl, parts, st);
+    if (err) return err;
+    err = smx_shard_pack(tin, &s, p, ctl, parts, send, st);
+    if (err) return err;
+    const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)s.ld;
+    err = nccl_err(ncclAllGather(send, recv, slot, ncclFloat64, comm, st));
+    if (err) return err;
+    if (e0) (void)hipEventRecord(e0, st);
+    err = smx_shard_update(tin, tout, recv, nranks, &s, p, ctl, log, log_cap, st);
+    if (e1) (void)hipEventRecord(e1, st);
+    return err;
+}
+}  // namespace
+
+int smx_shard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                  smx_ctl* ctl, smx_part* parts, double* send, double* recv, int32_t nranks,
+                  void* comm, int32_t* log, int64_t log_cap, void* stream) {
+    if (!shape_ok(shape) || !comm || nranks < 1 || k < 0) return (int)hipErrorInvalidValue;
+    for (int step = 0; step < k; ++step) {
+        const int p = (parity + step) & 1;
+        const int err = shard_pivot(p ? buf1 : buf0, p ? buf0 : buf1, *shape, p, ctl, parts,
+                                    send, recv, nranks, reinterpret_cast<ncclComm_t>(comm), log,
+                                    log_cap, nullptr, nullptr, S(stream));
+        if (err) return err;
+    }
+    return 0;
+}
+
+int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                        int32_t k, smx_ctl* ctl, smx_part* parts, double* send, double* recv,
+                        int32_t nranks, void* comm, int32_t* log, int64_t log_cap, void* stream,
+                        float* host_update_ms, float* host_total_ms) {
+    if (!shape_ok(shape) || !comm || nranks < 1 || k < 1 || !host_update_ms || !host_total_ms)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    hipEvent_t* ev = new hipEvent_t[2 * (size_t)k + 1];
+    for (int i = 0; i < 2 * k + 1; ++i) {
+        if (hipEventCreate(&ev[i]) != hipSuccess) {
+            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+            delete[] ev;
+            return (int)hipErrorOutOfMemory;
+        }
+    }
+    (void)hipEventRecord(ev[2 * k], st);
+    int err = 0;
+    for (int step = 0; step < k && !err; ++step) {
+        const int p = (parity + step) & 1;
+        err = shard_pivot(p ? buf1 : buf0, p ? buf0 : buf1, *shape, p, ctl, parts, send, recv,
+                          nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap, ev[2 * step],
+                          ev[2 * step + 1], st);
+    }
+    if (!err) err = (int)hipEventSynchronize(ev[2 * k - 1]);
+    if (!err) {
+        for (int step = 0; step < k; ++step)
+            (void)hipEventElapsedTime(&host_update_ms[step], ev[2 * step], ev[2 * step + 1]);
+        (void)hipEventElapsedTime(host_total_ms, ev[2 * k], ev[2 * k - 1]);
+    }
+    for (int i = 0; i < 2 * k + 1; ++i) (void)hipEventDestroy(ev[i]);
+    delete[] ev;
+    return err;
 }
 
 int smx_shard_begin(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,

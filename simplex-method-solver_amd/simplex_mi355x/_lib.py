@@ -44,7 +44,8 @@ _lib = None
 EXPORTS = (
     "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_set_xpos", "smx_reset", "smx_select", "smx_finalize", "smx_update",
     "smx_run", "smx_run_timed", "smx_graph_create", "smx_graph_launch", "smx_graph_destroy", "smx_update_forced",
-    "smx_batch_solve", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
+    "smx_batch_solve", "smx_comm_unique_id", "smx_comm_init", "smx_comm_destroy",
+    "smx_shard_run", "smx_shard_run_timed", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
     "smx_shard_finish",
 )
 
@@ -85,6 +86,14 @@ def load():
         "smx_shard_pack": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_merge": ([vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_shard_update": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
+        "smx_comm_unique_id": ([vp], ctypes.c_int),
+        "smx_comm_init": ([ctypes.POINTER(ctypes.c_void_p), i32, vp, i32], ctypes.c_int),
+        "smx_comm_destroy": ([vp], ctypes.c_int),
+        "smx_shard_run": ([vp, vp, sp, i32, i32, vp, vp, vp, vp, i32, vp, vp, i64, vp],
+                          ctypes.c_int),
+        "smx_shard_run_timed": ([vp, vp, sp, i32, i32, vp, vp, vp, vp, i32, vp, vp, i64, vp,
+                                 ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)],
+                                ctypes.c_int),
         "smx_batch_solve": ([vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp],
                             ctypes.c_int),
         "smx_shard_begin": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),

@@ -126,8 +126,8 @@ def load_device(path: str, device=None, row_lo: int = 0, row_hi: int | None = No
         dev.buf.zero_()
         for lo in range(0, rows, rows_per_chunk):
             hi = min(rows, lo + rows_per_chunk)
-            blk = torch.from_numpy(np.ascontiguousarray(mm[row_lo + lo:row_lo + hi, :C]))
+            blk = torch.from_numpy(np.array(mm[row_lo + lo:row_lo + hi, :C]))
             dev.buf[0, lo:hi, :C].copy_(blk)
-        dev.buf[0, rows, :C].copy_(torch.from_numpy(np.ascontiguousarray(mm[n, :C])))
+        dev.buf[0, rows, :C].copy_(torch.from_numpy(np.array(mm[n, :C])))
     dev.reset_state()
     return dev

@@ -38,6 +38,32 @@ def row_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return rank * n // world, (rank + 1) * n // world
 
 
+class RcclComm:
+    """This rank's own RCCL communicator for the native shard driver (smx_comm_*).
+
+    The 128-byte unique id is made on rank 0 and broadcast over the already-initialised
+    torch.distributed group; after that every collective of the pivot loop is issued by
+    libsmx.so on the solver stream (no torch stream hand-offs)."""
+
+    def __init__(self, group=None):
+        L = _lib.load()
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        uid = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            _lib.check(L.smx_comm_unique_id(uid), "smx_comm_unique_id")
+        box = [bytes(uid.raw)]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = ctypes.create_string_buffer(box[0], 128)
+        h = ctypes.c_void_p()
+        _lib.check(L.smx_comm_init(ctypes.byref(h), self.world, uid, self.rank), "smx_comm_init")
+        self.handle = h.value
+
+    def close(self):
+        if self.handle:
+            _lib.load().smx_comm_destroy(self.handle)
+            self.handle = None
+
+
 class HipShardBackend:
     """This rank's slice of the tableau in HBM plus the exchange buffers."""
 
@@ -74,6 +100,31 @@ class HipShardBackend:
         d.step += 1
         d._pending = True
 
+    def run_native(self, k: int, comm: "RcclComm") -> None:
+        """k pivots, all-gathers issued by libsmx.so on the solver stream (no host sync)."""
+        d = self.dev
+        _lib.check(_lib.load().smx_shard_run(
+            d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
+            d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(), self.recv.data_ptr(),
+            self.world, comm.handle, d.log.data_ptr(), d.log_cap, d.stream.cuda_stream),
+            "smx_shard_run")
+        d.step += k
+        d._pending = True
+
+    def run_native_timed(self, k: int, comm: "RcclComm"):
+        """Like run_native, with HIP events around every update kernel (synchronous)."""
+        d = self.dev
+        upd = (ctypes.c_float * k)()
+        tot = ctypes.c_float()
+        _lib.check(_lib.load().smx_shard_run_timed(
+            d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
+            d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(), self.recv.data_ptr(),
+            self.world, comm.handle, d.log.data_ptr(), d.log_cap, d.stream.cuda_stream, upd,
+            ctypes.byref(tot)), "smx_shard_run_timed")
+        d.step += k
+        d._pending = True
+        return np.frombuffer(upd, dtype=np.float32).copy(), float(tot.value)
+
     def state(self) -> dict:
         c = self.dev.sync_state()
         return {"npivots": int(c["npivots"]), "term": bool(c["term"]),
@@ -87,12 +138,17 @@ class HipShardBackend:
 
 
 class ShardedSolver:
-    """The per-pivot protocol over any backend with begin/finish/state and a send/recv pair."""
+    """The per-pivot protocol over any backend with begin/finish/state and a send/recv pair.
 
-    def __init__(self, backend, group=None, allgather=None):
+    With ``comm`` (an ``RcclComm``) and the HIP backend, ``run`` uses the native driver
+    (libsmx.so issues select / pack / ncclAllGather / update on the solver stream); otherwise each
+    pivot is begin -> torch.distributed all-gather -> finish (the path the gloo tests run)."""
+
+    def __init__(self, backend, group=None, allgather=None, comm=None):
         self.be = backend
         self.group = group
         self._allgather = allgather
+        self.comm = comm
 
     def _exchange(self) -> None:
         if self._allgather is not None:
@@ -108,8 +164,11 @@ class ShardedSolver:
             self.be.finish(ev_before, ev_after)
 
     def run(self, k: int) -> dict:
-        for _ in range(k):
-            self.pivot()
+        if self.comm is not None:
+            self.be.run_native(k, self.comm)
+        else:
+            for _ in range(k):
+                self.pivot()
         return self.be.state()
 
 
@@ -135,21 +194,15 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     be = HipShardBackend(local, n, m, m, lo, world, device=device,
                          log_cap=max(1 << 16, args.warmup + args.steps))
     del local
-    solver = ShardedSolver(be)
+    comm = RcclComm()
+    solver = ShardedSolver(be, comm=comm)
     if args.warmup:
         solver.run(args.warmup)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    with be.stream_ctx():
-        for a, b in evs:  # materialise the events before their handles go to the C side
-            a.record(be.dev.stream)
-            b.record(be.dev.stream)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for a, b in evs:
-        solver.pivot(a, b)
+    upd_ms, _ = be.run_native_timed(args.steps, comm)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -163,7 +216,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
             if tr.pivot(int(r), int(c)):
                 cycle = {"first_step": tr.cycle[0], "period": tr.cycle[1]}
                 break
-    upd_ms = np.array([a.elapsed_time(b) for a, b in evs], dtype=np.float64)
+    upd_ms = np.asarray(upd_ms, dtype=np.float64)
     stats = torch.tensor([elapsed, float(upd_ms.mean()),
                           float(st["npivots"] == args.warmup + args.steps and not st["term"])],
                          dtype=torch.float64, device=device)
@@ -193,7 +246,8 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
             "data": "synthetic: seeded dense random LP, each rank generates its own row block "
                     "on the host and uploads it to its HBM before timing (no dataset)",
             "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
-                       "parallelism": f"row-shard x{world} (1 all-gather per pivot, RCCL)",
+                       "parallelism": f"row-shard x{world} (1 RCCL all-gather per pivot, "
+                                      "issued natively on the solver stream)",
                        "rows_per_rank": hi - lo, "kernels_per_pivot": 3,
                        "collectives_per_pivot": 1},
             "hbm_gbs_per_pivot": 16.0 * R * C / (wall / args.steps) / 1e9,
@@ -209,6 +263,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
         }
         print(json.dumps(out), flush=True)
     dist.barrier()
+    comm.close()
     dist.destroy_process_group()
 
 

@@ -82,3 +82,14 @@ def test_hip_shards_terminal_outcome():
     for s in states:
         assert s["term"] and s["status"] == st and s["npivots"] == done
     assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))
+
+
+def test_native_rccl_driver_world1():
+    """libsmx.so's own RCCL communicator + stream-ordered all-gather (1-rank job)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(repo, "tools", "check_native_shard.py")],
+                         capture_output=True, text=True, timeout=600, cwd=repo)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
