@@ -67,10 +67,11 @@ typedef struct smx_ctl {
     int32_t xpos[2][2]; /* [parity][x1, x2]: position code of labels 'x1', 'x2' (simplex.py:
                            58-59): p >= 0 row p (basic), -(j+1) column j, SMX_ABSENT none      */
     int64_t npiv[2];    /* [parity]: pivot index of the step (history ring position)          */
-    int64_t reserved[4];
+    int32_t dec[2][4];  /* reserved (zero)                                                    */
 } smx_ctl; /* 128 bytes */
 
-/* One per select workgroup (caller allocates nparts * sizeof(smx_part) bytes). */
+/* One per select workgroup (caller allocates 2 * nparts * sizeof(smx_part) bytes: the fused
+ * chain double-buffers them by parity; the unfused calls use the first nparts). */
 typedef struct smx_part {
     int32_t p1col;    /* phase 1: first column j with T[r][j] > 0 in this workgroup's slice  */
     int32_t first;    /* phase 2: first row with T[i][c] != 0 (its ratio may be NaN)         */
@@ -114,6 +115,14 @@ int smx_set_xpos(smx_ctl* ctl, int32_t parity, int32_t x1code, int32_t x2code, v
 /* pick_element, part 1: per-workgroup partials of the selection for the tableau T. */
 int smx_select(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                smx_part* parts, void* stream);
+
+/* Fused chain (default for smx_run / smx_run_timed / smx_graph_*): ONE kernel per pivot --
+ * the update of step k, whose first nparts workgroups also compute step k+1's select inputs
+ * (first negative new "-b" row, entering column, ratio-test partials) from T_k with the update's
+ * own arithmetic (bit-identical); a chain is primed by one small kernel and ends with a one-wave
+ * publish of ctl->negb.  Records are double-buffered: `parts` must hold 2 * nparts of them.
+ * smx_tune_fused(0) restores the select + update pair; returns the previous setting. */
+int smx_tune_fused(int32_t on);
 
 /* pick_element, part 2: reduce the partials into ctl->sel_* (does not set term, logs nothing). */
 int smx_finalize(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,

@@ -31,7 +31,7 @@
 static_assert(sizeof(smx_ctl) == 128, "smx_ctl layout");
 static_assert(offsetof(smx_ctl, term) == 16 && offsetof(smx_ctl, npivots) == 40 &&
                   offsetof(smx_ctl, shard_off) == 56 && offsetof(smx_ctl, xpos) == 64 &&
-                  offsetof(smx_ctl, npiv) == 80,
+                  offsetof(smx_ctl, npiv) == 80 && offsetof(smx_ctl, dec) == 96,
               "smx_ctl offsets (mirrored in simplex_mi355x/_lib.py)");
 static_assert(sizeof(smx_part) == 32, "smx_part layout");
 
@@ -423,6 +423,220 @@ __global__ __launch_bounds__(kWave) void k_finalize(const smx_part* __restrict__
 }
 
 // ---------------------------------------------------------------------------------------------
+// Look-ahead selection (fused chain): the whole pick_element of step k+1 (simplex.py:70-141)
+// computed by ONE workgroup from T_k and step k's pivot (r, c), while the other workgroups write
+// T_{k+1}.  Every entry it needs of T_{k+1} is re-derived with the update's own expression
+// (nv below), so the decision is bit-identical to selecting on the materialised T_{k+1}.
+__device__ __forceinline__ double nv(const double* __restrict__ T, int64_t ld, int r, int c,
+                                     double e, const double* __restrict__ prow, int i, int j,
+                                     double pci) {
+    const double x = T[(int64_t)i * ld + j];
+    double num;
+    if (i == r) {
+        num = (j == c) ? 1.0 : -x;
+    } else {
+        const double a = x * e;
+        const double b = prow[j] * pci;
+        num = (j == c) ? x : (a - b);
+    }
+    return num / e;
+}
+
+template <int NT>
+__device__ __forceinline__ int block_min_int(int x, int* s_tmp) {
+    x = wave_min_int(x);
+    const int wid = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_tmp[wid] = x;
+    __syncthreads();
+    int r = s_tmp[0];
+#pragma unroll
+    for (int w = 1; w < NT / kWave; ++w) r = min(r, s_tmp[w]);
+    return r;
+}
+
+// Fused chain: the select inputs of the NEXT step, computed by nparts workgroups from T_k and
+// step k's pivot (APPLY) -- or from T_k itself to prime a chain (!APPLY).  Workgroup b covers rows
+// b*NT + tid + q*nparts*NT and writes one record:
+//   p1col  first row of its slice whose new "-b" entry is negative (simplex.py:72-76), or NONE
+//   first/first_v, best_*  its ratio-test candidates on the new entering column (:105-141)
+// and workgroup 0 stores the entering column itself (first negative new f-row coefficient,
+// simplex.py:94-98) in ctl->negf[slot].  Nothing is min-ed atomically, so no slot needs a reset.
+template <int NT, bool APPLY>
+__device__ void la_partial(const double* __restrict__ T, int64_t ld, int n, int m, int fscan,
+                           int r, int c, double e, const double* __restrict__ prow,
+                           smx_part* __restrict__ out, int b, int nparts,
+                           smx_ctl* __restrict__ ctl, int slot) {
+    __shared__ int s_tmp[NT / kWave];
+    __shared__ int s_b[NT / kWave];
+    __shared__ First s_f[NT / kWave];
+    __shared__ Cand s_c[NT / kWave];
+    const int tid = threadIdx.x;
+    auto val = [&](int i, int j, double pci) -> double {
+        if (APPLY) return nv(T, ld, r, c, e, prow, i, j, pci);
+        return T[(int64_t)i * ld + j];
+    };
+    int nf = SMX_NONE;
+    const double pcf = APPLY ? T[(int64_t)n * ld + c] : 0.0;
+    for (int j = tid; j < fscan; j += NT) {
+        if (val(n, j, pcf) < 0.0) {
+            nf = j;
+            break;
+        }
+    }
+    nf = block_min_int<NT>(nf, s_tmp);
+    int nb = SMX_NONE;
+    First f{SMX_NONE, 0.0};
+    Cand bc = cand_none();
+    for (int i = b * NT + tid; i < n; i += nparts * NT) {
+        const double pci = APPLY ? T[(int64_t)i * ld + c] : 0.0;
+        const double bv = val(i, m, pci);
+        if (bv < 0.0 && i < nb) nb = i;
+        if (nf != SMX_NONE) {
+            const double a = val(i, nf, pci);
+            if (a != 0.0) {
+                const double v = bv / a;
+                if (i < f.idx) {
+                    f.idx = i;
+                    f.v = v;
+                }
+                if (!isnan(v)) {
+                    const Cand x = classify(v, i);
+                    if (better(x, bc)) bc = x;
+                }
+            }
+        }
+    }
+    nb = wave_min_int(nb);
+    f = wave_first(f);
+    bc = wave_best(bc);
+    const int wid = tid >> 6;
+    if ((tid & 63) == 0) {
+        s_b[wid] = nb;
+        s_f[wid] = f;
+        s_c[wid] = bc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < NT / kWave; ++w) {
+            nb = min(nb, s_b[w]);
+            if (s_f[w].idx < f.idx) f = s_f[w];
+            if (better(s_c[w], bc)) bc = s_c[w];
+        }
+        smx_part pt;
+        pt.p1col = nb;
+        pt.first = f.idx;
+        pt.first_v = f.v;
+        pt.best_cls = bc.cls;
+        pt.best_i = bc.idx;
+        pt.best_v = bc.v;
+        out[b] = pt;
+        if (b == 0) ctl->negf[slot] = nf;
+    }
+}
+
+// Fused-chain decision of step k (simplex.py:70-141) from its look-ahead records and T_k: the
+// phase-1 row is the minimum of the records' p1col; its first positive entry is scanned by the
+// whole block on the materialised T_k (:81-85); phase 2 reduces the ratio partials (:105-141).
+template <int NT>
+__device__ Decision decide_fused(const smx_ctl* __restrict__ ctl,
+                                 const smx_part* __restrict__ parts, int nparts, int parity,
+                                 int n, int m, int flen, const double* __restrict__ T, int64_t ld,
+                                 int* negb_out) {
+    __shared__ int s_tmp[NT / kWave];
+    __shared__ int s_negb;
+    __shared__ Decision s_d;
+    const int tid = threadIdx.x;
+    if (tid < kWave) {
+        int nb = SMX_NONE;
+        for (int k = tid; k < nparts; k += kWave) nb = min(nb, parts[k].p1col);
+        nb = wave_min_int(nb);
+        if (tid == 0) s_negb = nb;
+    }
+    __syncthreads();
+    const int negb = s_negb;
+    *negb_out = negb;
+    if (negb != SMX_NONE) {
+        const double* row = T + (int64_t)negb * ld;
+        int p1 = SMX_NONE;
+        for (int j = tid; j < m; j += NT) {
+            if (row[j] > 0.0) {
+                p1 = j;
+                break;
+            }
+        }
+        p1 = block_min_int<NT>(p1, s_tmp);
+        Decision d;
+        d.r = negb;
+        d.c = p1;
+        d.status = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
+        return d;
+    }
+    if (tid < kWave) {
+        Decision d;
+        const int c = ctl->negf[parity];
+        d.c = c;
+        d.r = SMX_NONE;
+        if (c == SMX_NONE) {
+            d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
+        } else {
+            First f{SMX_NONE, 0.0};
+            Cand b = cand_none();
+            for (int k = tid; k < nparts; k += kWave) {
+                const smx_part p = parts[k];
+                if (p.first < f.idx) {
+                    f.idx = p.first;
+                    f.v = p.first_v;
+                }
+                Cand o{p.best_cls, p.best_i, p.best_v};
+                if (better(o, b)) b = o;
+            }
+            f = wave_first(f);
+            b = wave_best(b);
+            if (f.idx == SMX_NONE) {
+                d.status = SMX_NOT_CONVERGE;
+            } else if (isnan(f.v)) {
+                d.status = SMX_PIVOT;
+                d.r = f.idx;
+            } else if (b.cls >= 2) {
+                d.status = SMX_NOT_CONVERGE;
+            } else {
+                d.status = SMX_PIVOT;
+                d.r = b.idx;
+            }
+        }
+        if (tid == 0) s_d = d;
+    }
+    __syncthreads();
+    return s_d;
+}
+
+// Prime a fused chain: the look-ahead records of step `parity` from T itself.
+__global__ __launch_bounds__(kUpdBlock) void k_la_prime(const double* __restrict__ T, int64_t ld,
+                                                        int n, int m, int fscan, int parity,
+                                                        smx_ctl* __restrict__ ctl,
+                                                        smx_part* __restrict__ parts) {
+    if (ctl->term) return;
+    la_partial<kUpdBlock, false>(T, ld, n, m, fscan, 0, 0, 1.0, T, parts, blockIdx.x, gridDim.x,
+                                 ctl, parity);
+}
+
+// End of a fused chain: publish the next step's first-negative-b row into ctl->negb[parity]
+// (the entering column is already in ctl->negf[parity]) so the unfused calls continue from it.
+__global__ __launch_bounds__(kWave) void k_publish(const smx_part* __restrict__ parts, int nparts,
+                                                   int parity, smx_ctl* __restrict__ ctl) {
+    if (ctl->term) return;
+    int nb = SMX_NONE;
+    for (int k = threadIdx.x; k < nparts; k += kWave) nb = min(nb, parts[k].p1col);
+    nb = wave_min_int(nb);
+    if (threadIdx.x == 0) {
+        ctl->negb[parity] = nb;
+        ctl->negb[parity ^ 1] = SMX_NONE;
+        ctl->negf[parity ^ 1] = SMX_NONE;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_update: the modified Jordan step (simplex.py:149-177), out of place.
 //
 // Streaming shape (measured on MI355X with tools/hbm_probe.hip: a grid-wide sweep in address
@@ -436,7 +650,7 @@ __global__ __launch_bounds__(kWave) void k_finalize(const smx_part* __restrict__
 //                    : (j == c ? x   : x*e - pr*pc) steps 2 and 4
 //     out = num / e
 // which is exactly the value the reference leaves in new_table[i][j] after steps 1-4.
-enum UpdMode { kSingle = 0, kShard = 1, kForced = 2 };
+enum UpdMode { kSingle = 0, kShard = 1, kForced = 2, kFused = 3 };
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
@@ -507,14 +721,24 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         r = forced_r;
         c = forced_c;
         prow = Tin + (int64_t)r * ld;
-    } else if (MODE == kSingle) {
+    } else if (MODE == kSingle || MODE == kFused) {
+        Decision dd;
+        int negb_f = SMX_NONE;
+        if (MODE == kFused)   // whole block (phase-1 row scan); parts = this step's slot
+            dd = decide_fused<kUpdBlock>(ctl, parts + (size_t)parity * nparts, nparts, parity,
+                                         n, m, flen, Tin, ld, &negb_f);
         if (tid < kWave) {
-            const Decision d = decide_from_parts(ctl, parts, nparts, parity, n, m, flen);
+            Decision d;
+            if (MODE == kFused)
+                d = dd;
+            else
+                d = decide_from_parts(ctl, parts, nparts, parity, n, m, flen);
             if (tid == 0) {
                 s_dec[0] = d.status;
                 s_dec[1] = d.r;
                 s_dec[2] = d.c;
                 if (blockIdx.x == 0) {
+                    if (MODE == kFused) ctl->negb[parity] = negb_f;   // host-visible state
                     ctl->sel_status = d.status;
                     ctl->sel_r = d.r;
                     ctl->sel_c = d.c;
@@ -565,7 +789,13 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     // history: rows whose new "-b" entry is x1 / x2 of the new tableau (find_optimum)
     int hx0 = -1, hx1 = -1;
     int64_t hslot = 0;
-    if (MODE == kSingle && xhist != nullptr && log_cap > 0) {
+    if (MODE == kFused && blockIdx.x < nparts) {
+        // this workgroup's share of step k+1's select partials (one kernel per pivot)
+        la_partial<kUpdBlock, true>(Tin, ld, n, m, fscan, r, c, e, prow,
+                                    const_cast<smx_part*>(parts) + (size_t)(parity ^ 1) * nparts,
+                                    blockIdx.x, nparts, ctl, parity ^ 1);
+    }
+    if ((MODE == kSingle || MODE == kFused) && xhist != nullptr && log_cap > 0) {
         hx0 = move_label(ctl->xpos[parity][0], r, c);
         hx1 = move_label(ctl->xpos[parity][1], r, c);
         hslot = 2 * (ctl->npiv[parity] % log_cap);
@@ -612,11 +842,13 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
                 else
                     o[h] = num / e;
                 if (MODE != kForced && jj < C) {
-                    if (MODE == kSingle && jj == m) {
+                    if ((MODE == kSingle || MODE == kFused) && jj == m) {
                         if (i == hx0) xhist[hslot] = o[h];
                         if (i == hx1) xhist[hslot + 1] = o[h];
                     }
-                    if (i < rows_local) {
+                    if (MODE == kFused) {
+                        // next-step scans come from the look-ahead records
+                    } else if (i < rows_local) {
                         if (jj == m && o[h] < 0.0) lb = min(lb, row0 + i);
                     } else if (jj < fscan && o[h] < 0.0) {
                         lf = min(lf, jj);
@@ -637,7 +869,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
             fetch(cur);
         }
     }
-    if (MODE != kForced) {
+    if (MODE == kSingle || MODE == kShard) {
         lb = wave_min_int(lb);
         lf = wave_min_int(lf);
         if (lane == 0) {
@@ -895,6 +1127,22 @@ int launch_select(const double* T, const smx_shape& s, int parity, smx_ctl* ctl,
     return (int)hipGetLastError();
 }
 
+// Fused chain helpers: prime the look-ahead records of step `parity` from T; publish at the end.
+int launch_prime(const double* T, const smx_shape& s, int parity, smx_ctl* ctl, smx_part* parts,
+                 hipStream_t st) {
+    const int fscan = s.flen < s.m ? s.flen : s.m;
+    hipLaunchKernelGGL(k_la_prime, dim3(s.nparts), dim3(kUpdBlock), 0, st, T, s.ld, s.n, s.m,
+                       fscan, parity, ctl, parts + (size_t)parity * s.nparts);
+    return (int)hipGetLastError();
+}
+
+int launch_publish(const smx_shape& s, int parity, smx_ctl* ctl, const smx_part* parts,
+                   hipStream_t st) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(kWave), 0, st, parts + (size_t)parity * s.nparts,
+                       s.nparts, parity, ctl);
+    return (int)hipGetLastError();
+}
+
 // ---- update-kernel variants (rows per unit TR, doubles per lane VEC, non-temporal stores) -----
 struct UpdVariant {
     int u, nts, ntl, pipe;
@@ -1005,7 +1253,9 @@ int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int 
                        int64_t log_cap, const double* recv, int fr, int fc, hipStream_t st) {
     const int v = g_variant;
     UpdFn fn = upd_fn<MODE>(v);
-    hipLaunchKernelGGL(fn, dim3(update_grid(s, v, (const void*)fn)), dim3(kUpdBlock), 0, st, Tin,
+    int grid = update_grid(s, v, (const void*)fn);
+    if (MODE == kFused && grid < s.nparts) grid = s.nparts;   // every partial slot is written
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, Tin,
                        Tout, s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl,
                        parts, s.nparts, log, xhist, log_cap, recv, fr, fc);
     return (int)hipGetLastError();
@@ -1018,8 +1268,22 @@ int launch_update(const double* Tin, double* Tout, const smx_shape& s, int parit
                                        nullptr, 0, 0, st);
 }
 
+int g_fused = 1;   // one kernel per pivot in chains (smx_tune_fused)
+
 int launch_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, smx_ctl* ctl,
                  smx_part* parts, int32_t* log, double* xhist, int64_t log_cap, hipStream_t st) {
+    if (g_fused && k > 0) {
+        // prime the records of the first step, one fused kernel per pivot, publish the next
+        int err = launch_prime(parity ? buf1 : buf0, s, parity, ctl, parts, st);
+        if (err) return err;
+        for (int step = 0; step < k; ++step) {
+            const int p = (parity + step) & 1;
+            err = launch_update_mode<kFused>(p ? buf1 : buf0, p ? buf0 : buf1, s, p, ctl, parts,
+                                             log, xhist, log_cap, nullptr, 0, 0, st);
+            if (err) return err;
+        }
+        return launch_publish(s, (parity + k) & 1, ctl, parts, st);
+    }
     for (int step = 0; step < k; ++step) {
         const int p = (parity + step) & 1;
         double* tin = p ? buf1 : buf0;
@@ -1063,6 +1327,12 @@ int smx_tune_set(int32_t variant, int32_t blocks_per_cu_override) {
     if (variant >= 0) g_variant = variant;
     if (blocks_per_cu_override >= 0) g_blocks_per_cu = blocks_per_cu_override;
     return 0;
+}
+
+int smx_tune_fused(int32_t on) {
+    const int prev = g_fused;
+    if (on >= 0) g_fused = on ? 1 : 0;
+    return prev;
 }
 
 int smx_tune_get(int32_t* variant, int32_t* blocks_per_cu_override, int32_t* nvariants,
@@ -1138,16 +1408,25 @@ int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
         }
     }
     (void)hipEventRecord(ev[2 * k], st);
+    if (g_fused) err = launch_prime(p0 ? buf1 : buf0, *shape, p0, ctl, parts, st);
     for (int step = 0; step < k && !err; ++step) {
         const int p = (p0 + step) & 1;
         double* tin = p ? buf1 : buf0;
         double* tout = p ? buf0 : buf1;
+        if (g_fused) {
+            (void)hipEventRecord(ev[2 * step], st);
+            err = launch_update_mode<kFused>(tin, tout, *shape, p, ctl, parts, log, xhist,
+                                             log_cap, nullptr, 0, 0, st);
+            (void)hipEventRecord(ev[2 * step + 1], st);
+            continue;
+        }
         err = launch_select(tin, *shape, p, ctl, parts, st);
         if (err) break;
         (void)hipEventRecord(ev[2 * step], st);
         err = launch_update(tin, tout, *shape, p, ctl, parts, log, xhist, log_cap, st);
         (void)hipEventRecord(ev[2 * step + 1], st);
     }
+    if (!err && g_fused) err = launch_publish(*shape, (p0 + k) & 1, ctl, parts, st);
     if (!err) err = (int)hipEventSynchronize(ev[2 * k - 1]);
     if (!err) {
         for (int step = 0; step < k; ++step)

@@ -26,7 +26,7 @@ CTL_DTYPE = np.dtype([
     ("negb", "<i4", (2,)), ("negf", "<i4", (2,)), ("term", "<i4"), ("sel_status", "<i4"),
     ("sel_r", "<i4"), ("sel_c", "<i4"), ("sel_e", "<f8"), ("npivots", "<i8"),
     ("sel_owner", "<i4"), ("pad0", "<i4"), ("shard_off", "<i8"), ("xpos", "<i4", (2, 2)),
-    ("npiv", "<i8", (2,)), ("reserved", "<i8", (4,)),
+    ("npiv", "<i8", (2,)), ("dec", "<i4", (2, 4)),
 ])
 ABSENT = -0x80000000
 assert CTL_DTYPE.itemsize == CTL_BYTES
@@ -42,7 +42,8 @@ class Shape(ctypes.Structure):
 _lib = None
 
 EXPORTS = (
-    "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_set_xpos", "smx_reset", "smx_select", "smx_finalize", "smx_update",
+    "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_tune_fused",
+    "smx_set_xpos", "smx_reset", "smx_select", "smx_finalize", "smx_update",
     "smx_run", "smx_run_timed", "smx_graph_create", "smx_graph_launch", "smx_graph_destroy", "smx_update_forced",
     "smx_batch_solve", "smx_comm_unique_id", "smx_comm_init", "smx_comm_destroy",
     "smx_shard_run", "smx_shard_run_timed", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
@@ -68,6 +69,7 @@ def load():
         "smx_version": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
         "smx_nparts_for": ([i32, i32], ctypes.c_int),
         "smx_tune_set": ([i32, i32], ctypes.c_int),
+        "smx_tune_fused": ([i32], ctypes.c_int),
         "smx_tune_get": ([ctypes.POINTER(i32)] * 6, ctypes.c_int),
         "smx_reset": ([vp, sp, i32, i32, vp, vp], ctypes.c_int),
         "smx_select": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),

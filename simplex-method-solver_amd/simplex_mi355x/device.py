@@ -68,7 +68,8 @@ class DeviceTableau:
         with torch.cuda.stream(self.stream):
             self.buf = torch.zeros((2, rows + 1, self.ld), dtype=torch.float64, device=self.device)
             self.ctl = torch.zeros(_lib.CTL_BYTES // 8, dtype=torch.int64, device=self.device)
-            self.parts = torch.zeros(self.nparts * _lib.PART_BYTES // 8, dtype=torch.int64,
+            # 2 x nparts: the fused chain double-buffers the partials by parity
+            self.parts = torch.zeros(2 * self.nparts * _lib.PART_BYTES // 8, dtype=torch.int64,
                                      device=self.device)
             self.log = torch.zeros(2 * log_cap, dtype=torch.int32, device=self.device)
             self.xhist = torch.zeros(2 * log_cap, dtype=torch.float64, device=self.device)

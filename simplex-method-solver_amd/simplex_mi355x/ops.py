@@ -48,11 +48,11 @@ def _bytes_ok(t: Tensor, nbytes: int, name: str) -> None:
         raise ValueError(f"{name}: needs a contiguous CUDA buffer of >= {nbytes} bytes")
 
 
-def _parts_ok(parts: Tensor, shape) -> None:
+def _parts_ok(parts: Tensor, shape, slots: int = 1) -> None:
     nparts = int(shape[6])
     if not 1 <= nparts <= 64:
         raise ValueError(f"nparts={nparts} out of range [1, 64]")
-    _bytes_ok(parts, nparts * _lib.PART_BYTES, "parts")
+    _bytes_ok(parts, slots * nparts * _lib.PART_BYTES, "parts")
 
 
 def _log_cap(log: Tensor) -> int:
@@ -125,7 +125,7 @@ def run(buf: Tensor, ctl: Tensor, parts: Tensor, log: Tensor, xhist: Tensor, sha
         raise ValueError("buf must be (2, R, ld)")
     _table_ok(buf[0], shape, "buf[0]")
     _bytes_ok(ctl, _lib.CTL_BYTES, "ctl")
-    _parts_ok(parts, shape)
+    _parts_ok(parts, shape, 2)      # the fused chain double-buffers the partials
     _xhist_ok(xhist, log)
     sh = make_shape(shape)
     _lib.check(_lib.load().smx_run(_ptr(buf[0]), _ptr(buf[1]), ctypes.byref(sh), parity, k,

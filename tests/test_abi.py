@@ -45,8 +45,8 @@ def test_struct_layouts_match_header():
     assert _lib.CTL_DTYPE.itemsize == 128
     # offsets used by the host and the kernels (include/smx.h)
     f = _lib.CTL_DTYPE.fields
-    assert (f["term"][1], f["npivots"][1], f["shard_off"][1], f["xpos"][1], f["npiv"][1]) == \
-        (16, 40, 56, 64, 80)
+    assert (f["term"][1], f["npivots"][1], f["shard_off"][1], f["xpos"][1], f["npiv"][1],
+            f["dec"][1]) == (16, 40, 56, 64, 80, 96)
 
 
 def test_host_helpers_without_gpu():

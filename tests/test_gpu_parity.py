@@ -334,3 +334,30 @@ def test_from_file_txt_and_smx(tmp_path):
     assert np.array_equal(np.array(ra[-1].table[n]).view(np.int64),
                           np.array(rb[-1].table[n]).view(np.int64))
     assert np.array_equal(np.array(ra[0].table[:n]).view(np.int64), T[:n].view(np.int64))
+
+
+# ----------------------------------------------------------------------------------------------
+# 10. the fused chain (look-ahead selection inside the update kernel) == the select+update chain
+def test_fused_chain_matches_unfused_on_every_fixture():
+    import simplex
+    from simplex_mi355x import _lib
+    L = _lib.load()
+    n_checked = 0
+    try:
+        for label, cons, func, rec in CASES:
+            if len(func) not in (len(cons[0]) - 1, len(cons[0])) or len(func) < 2:
+                continue
+            runs = []
+            for fused in (1, 0):
+                L.smx_tune_fused(fused)
+                sm = simplex.SimplexMethod([list(r) for r in cons], list(func))
+                out = sm.solve(record_history=False, max_pivots=trajectory_cap(rec), chunk=5)
+                runs.append((sm.pivot_log, sm.status, table_hash(out[-2 if sm.status == "error"
+                                                                    else -1].table)))
+            assert runs[0] == runs[1], label
+            exp = [(s["i"], s["j"]) for s in rec["steps"][:-1]]
+            assert runs[0][0] == exp[:len(runs[0][0])], label
+            n_checked += 1
+    finally:
+        L.smx_tune_fused(1)
+    assert n_checked > 250
