@@ -109,7 +109,7 @@ def cpu_baseline(T, n, m, seconds):
 def run_single(args):
     import numpy as np
     import torch
-    from simplex_mi355x import lp
+    from simplex_mi355x import _lib, lp
     from simplex_mi355x.device import DeviceTableau
 
     n, m = shape_of(args)
@@ -129,6 +129,7 @@ def run_single(args):
     valid = done == args.warmup + args.steps and not ctl["term"]
     cycle = cycle_report(n, m, dev.read_log(0, done))
     bytes_per_pivot = 16.0 * R * C
+    fused = _lib.fused_enabled()   # one k_update<kFused> per pivot, else k_select + k_update
     avg_upd = float(np.mean(upd_ms)) * 1e-3
     achieved = bytes_per_pivot / avg_upd / 1e9
     workload = f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
@@ -148,12 +149,12 @@ def run_single(args):
         "data": "synthetic: seeded dense random LP generated on the host, uploaded to HBM "
                 "before timing (no dataset)",
         "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
-                   "parallelism": "single GPU", "kernels_per_pivot": 2},
+                   "parallelism": "single GPU", "kernels_per_pivot": 1 if fused else 2},
         "hbm_gbs_per_pivot": bytes_per_pivot / (wall / args.steps) / 1e9,
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                      "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                     "kernel": "k_update<kSingle>",
+                     "kernel": "k_update<kFused>" if fused else "k_update<kSingle>",
                      "algorithmic_bytes_per_launch": bytes_per_pivot,
                      "avg_kernel_ms": avg_upd * 1e3},
         "trajectory_valid": bool(valid),

@@ -99,7 +99,9 @@ int smx_nparts_for(int32_t rows, int32_t m);
 
 /* Tuning of the update kernel (process-wide): variant index (16-B loads in flight per lane,
  * non-temporal stores; see smx_tune_get) and resident blocks per CU (0 = occupancy API).
- * A negative argument keeps the current value. */
+ * -1 keeps the current value; variant -2 restores the automatic choice (the default: plain
+ * loads for a tableau buffer of at most 16 MiB, which stays cache-resident, non-temporal
+ * loads above).  smx_tune_get reports variant -1 while automatic. */
 int smx_tune_set(int32_t variant, int32_t blocks_per_cu);
 int smx_tune_get(int32_t* variant, int32_t* blocks_per_cu, int32_t* nvariants,
                  int32_t* units_in_flight, int32_t* vec, int32_t* nt);

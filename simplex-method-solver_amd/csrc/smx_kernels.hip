@@ -544,56 +544,35 @@ __device__ Decision decide_fused(const smx_ctl* __restrict__ ctl,
                                  int n, int m, int flen, const double* __restrict__ T, int64_t ld,
                                  int* negb_out) {
     __shared__ int s_tmp[NT / kWave];
-    __shared__ int s_negb;
     __shared__ Decision s_d;
+    __shared__ int s_negb;
     const int tid = threadIdx.x;
     if (tid < kWave) {
-        int nb = SMX_NONE;
-        for (int k = tid; k < nparts; k += kWave) nb = min(nb, parts[k].p1col);
-        nb = wave_min_int(nb);
-        if (tid == 0) s_negb = nb;
-    }
-    __syncthreads();
-    const int negb = s_negb;
-    *negb_out = negb;
-    if (negb != SMX_NONE) {
-        const double* row = T + (int64_t)negb * ld;
-        int p1 = SMX_NONE;
-        for (int j = tid; j < m; j += NT) {
-            if (row[j] > 0.0) {
-                p1 = j;
-                break;
-            }
-        }
-        p1 = block_min_int<NT>(p1, s_tmp);
-        Decision d;
-        d.r = negb;
-        d.c = p1;
-        d.status = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
-        return d;
-    }
-    if (tid < kWave) {
-        Decision d;
+        // one pass over the records (nparts <= 64: one per lane) and the entering column
         const int c = ctl->negf[parity];
+        int nb = SMX_NONE;
+        First f{SMX_NONE, 0.0};
+        Cand b = cand_none();
+        for (int k = tid; k < nparts; k += kWave) {
+            const smx_part p = parts[k];
+            nb = min(nb, p.p1col);
+            if (p.first < f.idx) {
+                f.idx = p.first;
+                f.v = p.first_v;
+            }
+            Cand o{p.best_cls, p.best_i, p.best_v};
+            if (better(o, b)) b = o;
+        }
+        nb = wave_min_int(nb);
+        Decision d;
         d.c = c;
         d.r = SMX_NONE;
-        if (c == SMX_NONE) {
-            d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
-        } else {
-            First f{SMX_NONE, 0.0};
-            Cand b = cand_none();
-            for (int k = tid; k < nparts; k += kWave) {
-                const smx_part p = parts[k];
-                if (p.first < f.idx) {
-                    f.idx = p.first;
-                    f.v = p.first_v;
-                }
-                Cand o{p.best_cls, p.best_i, p.best_v};
-                if (better(o, b)) b = o;
-            }
+        if (nb == SMX_NONE) {          // phase 2 (the records were built for column c)
             f = wave_first(f);
             b = wave_best(b);
-            if (f.idx == SMX_NONE) {
+            if (c == SMX_NONE) {
+                d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
+            } else if (f.idx == SMX_NONE) {
                 d.status = SMX_NOT_CONVERGE;
             } else if (isnan(f.v)) {
                 d.status = SMX_PIVOT;
@@ -605,10 +584,30 @@ __device__ Decision decide_fused(const smx_ctl* __restrict__ ctl,
                 d.r = b.idx;
             }
         }
-        if (tid == 0) s_d = d;
+        if (tid == 0) {
+            s_negb = nb;
+            s_d = d;
+        }
     }
     __syncthreads();
-    return s_d;
+    const int negb = s_negb;
+    *negb_out = negb;
+    if (negb == SMX_NONE) return s_d;
+    // phase 1: first positive entry of the first-negative-b row of the materialised T_k
+    const double* row = T + (int64_t)negb * ld;
+    int p1 = SMX_NONE;
+    for (int j = tid; j < m; j += NT) {
+        if (row[j] > 0.0) {
+            p1 = j;
+            break;
+        }
+    }
+    p1 = block_min_int<NT>(p1, s_tmp);
+    Decision d;
+    d.r = negb;
+    d.c = p1;
+    d.status = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
+    return d;
 }
 
 // Prime a fused chain: the look-ahead records of step `parity` from T itself.
@@ -685,8 +684,17 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     constexpr int kChunk = kWave * 2;                  // doubles per unit
     const int nchunks = (C + kChunk - 1) / kChunk;
     const int64_t units = (int64_t)nchunks * R;
-    const int NW = gridDim.x * kUpdWaves;
-    const int w = blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(tid >> 6);
+    // kFused: workgroups [0, nparts) compute the look-ahead records; they join the sweep only
+    // when forced_r (= "look-ahead sweeps") is set: tableaux beyond the Infinity Cache, whose
+    // stream needs every resident wave's loads in flight (launch_update_mode)
+    const bool la_sweep = (MODE == kFused) && forced_r != 0;
+    const int lab = (MODE == kFused && !la_sweep) ? nparts : 0;
+    const bool la = (MODE == kFused) && (int)blockIdx.x < nparts;
+    const bool sweeps = !la || la_sweep;
+    const int NW = ((int)gridDim.x - lab) * kUpdWaves;
+    const int w = sweeps ? ((int)blockIdx.x - lab) * kUpdWaves +
+                               __builtin_amdgcn_readfirstlane(tid >> 6)
+                         : 0;
     // unit u = i * nchunks + ch; advancing u by NW advances (i, ch) by (qs, rs)
     const int qs = NW / nchunks, rs = NW % nchunks;
     int i_cur = w / nchunks, ch_cur = w % nchunks;
@@ -713,7 +721,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         }
     };
     Batch<U> cur;
-    fetch(cur);
+    if (sweeps) fetch(cur);
 
     int r, c;
     const double* prow;
@@ -789,11 +797,12 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     // history: rows whose new "-b" entry is x1 / x2 of the new tableau (find_optimum)
     int hx0 = -1, hx1 = -1;
     int64_t hslot = 0;
-    if (MODE == kFused && blockIdx.x < nparts) {
-        // this workgroup's share of step k+1's select partials (one kernel per pivot)
+    if (MODE == kFused && la) {
+        // this workgroup's share of step k+1's select inputs (one kernel per pivot)
         la_partial<kUpdBlock, true>(Tin, ld, n, m, fscan, r, c, e, prow,
                                     const_cast<smx_part*>(parts) + (size_t)(parity ^ 1) * nparts,
                                     blockIdx.x, nparts, ctl, parity ^ 1);
+        if (!la_sweep) return;
     }
     if ((MODE == kSingle || MODE == kFused) && xhist != nullptr && log_cap > 0) {
         hx0 = move_label(ctl->xpos[parity][0], r, c);
@@ -1155,7 +1164,15 @@ constexpr UpdVariant kVariants[] = {{2, 1, 0, 0}, {2, 1, 1, 0}, {2, 1, 0, 1}, {2
 constexpr int kFirstDiagVariant = 10;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 // Defaults from tools/tune_update.py on MI355X at 16384^2 (profiles/r01_tune_sweep*.jsonl).
-int g_variant = 1;        // U=2, nt stores + nt loads, 5 blocks/CU; smx_tune_set overrides
+// Variant -1 = automatic: U=2 with non-temporal stores and loads (1) for tableaux that stream
+// from HBM; plain loads (0) when one buffer is at most kCacheTable bytes, where the ping-pong
+// pair stays in the 256 MB Infinity Cache and a non-temporal load only adds latency
+// (profiles/r01_sweep_small.jsonl: 1024^2 11.1 vs 13.1 us per fused pivot; from 2048^2 on the
+// non-temporal variant is as fast or faster).
+int g_variant = -1;       // smx_tune_set overrides
+constexpr int kLargeVariant = 1, kSmallVariant = 0;
+constexpr int64_t kCacheTable = 16ll << 20;
+constexpr int64_t kLaSweepTable = 256ll << 20;
 int g_blocks_per_cu = 0;  // 0: kDefaultBpc, capped by the occupancy API (see blocks_per_cu)
 constexpr int kDefaultBpc = 5;
 
@@ -1179,6 +1196,11 @@ UpdFn upd_fn(int v) {
         case 10: return k_update<MODE, 2, true, true, false, true>;
         default: return k_update<MODE, 1, true, true, true, true>;
     }
+}
+
+int variant_for(const smx_shape& s) {
+    if (g_variant >= 0) return g_variant;
+    return (int64_t)(s.rows + 1) * s.ld * 8 <= kCacheTable ? kSmallVariant : kLargeVariant;
 }
 
 // Resident blocks per CU for a kernel, cached.  The grid is exactly CUs x this, so every block
@@ -1225,12 +1247,12 @@ int num_cus() {
 
 // Grid = resident blocks, trimmed so the wave count is a multiple of the chunks per row (then
 // every wave keeps one pivot-row slice for the whole sweep).
-int update_grid(const smx_shape& s, int variant, const void* fn) {
-    (void)variant;
+int update_grid(const smx_shape& s, const void* fn, int reserved) {
     const int64_t R = s.rows + 1;
     const int64_t nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
     const int64_t units = nchunks * R;
-    int64_t blocks = (int64_t)num_cus() * blocks_per_cu(fn);
+    int64_t blocks = (int64_t)num_cus() * blocks_per_cu(fn) - reserved;
+    if (blocks < 1) blocks = 1;
     // waves = a multiple of lcm(nchunks, waves per block) when that keeps >= 3/4 of them
     int64_t g = nchunks, h = kUpdWaves;
     while (h) {
@@ -1244,17 +1266,22 @@ int update_grid(const smx_shape& s, int variant, const void* fn) {
     const int64_t need = (units + kUpdWaves - 1) / kUpdWaves;
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
-    return (int)blocks;
+    return (int)blocks + reserved;
 }
 
 template <int MODE>
 int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int parity,
                        smx_ctl* ctl, const smx_part* parts, int32_t* log, double* xhist,
                        int64_t log_cap, const double* recv, int fr, int fc, hipStream_t st) {
-    const int v = g_variant;
+    const int v = variant_for(s);
     UpdFn fn = upd_fn<MODE>(v);
-    int grid = update_grid(s, v, (const void*)fn);
-    if (MODE == kFused && grid < s.nparts) grid = s.nparts;   // every partial slot is written
+    // kFused: the first nparts workgroups compute the look-ahead records; within the Infinity
+    // Cache they are reserved (their extra round trips would be the critical path), beyond it
+    // they sweep too (profiles/r01_sweep_small.jsonl)
+    const bool la_sweep = MODE == kFused && (int64_t)(s.rows + 1) * s.ld * 8 > kLaSweepTable;
+    int grid = update_grid(s, (const void*)fn, MODE == kFused && !la_sweep ? s.nparts : 0);
+    if (grid < s.nparts) grid = s.nparts;
+    if (MODE == kFused) fr = la_sweep ? 1 : 0;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, Tin,
                        Tout, s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl,
                        parts, s.nparts, log, xhist, log_cap, recv, fr, fc);
@@ -1324,7 +1351,7 @@ int smx_tune_set(int32_t variant, int32_t blocks_per_cu_override) {
         const char* env = getenv("SMX_ALLOW_DIAG");
         if (!env || env[0] != '1') return (int)hipErrorInvalidValue;
     }
-    if (variant >= 0) g_variant = variant;
+    if (variant >= 0 || variant == -2) g_variant = variant >= 0 ? variant : -1;
     if (blocks_per_cu_override >= 0) g_blocks_per_cu = blocks_per_cu_override;
     return 0;
 }
@@ -1340,10 +1367,10 @@ int smx_tune_get(int32_t* variant, int32_t* blocks_per_cu_override, int32_t* nva
     if (variant) *variant = g_variant;
     if (blocks_per_cu_override) *blocks_per_cu_override = g_blocks_per_cu;
     if (nvariants) *nvariants = kNumVariants;
-    if (units_in_flight) *units_in_flight = kVariants[g_variant].u;
+    const int gv = g_variant >= 0 ? g_variant : kLargeVariant;   // auto: report the HBM one
+    if (units_in_flight) *units_in_flight = kVariants[gv].u;
     if (vec) *vec = 2;
-    if (nt) *nt = kVariants[g_variant].nts | (kVariants[g_variant].ntl << 1) |
-                  (kVariants[g_variant].pipe << 2);
+    if (nt) *nt = kVariants[gv].nts | (kVariants[gv].ntl << 1) | (kVariants[gv].pipe << 2);
     return 0;
 }
 

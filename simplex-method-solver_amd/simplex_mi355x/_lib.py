@@ -115,6 +115,11 @@ def version() -> str:
     return buf.value.decode()
 
 
+def fused_enabled() -> bool:
+    """True when chains run one fused kernel per pivot (smx_tune_fused; the default)."""
+    return bool(load().smx_tune_fused(-1))
+
+
 def check(err: int, what: str) -> None:
     if err != 0:
         raise RuntimeError(f"{what} failed with hipError {err}")

@@ -52,19 +52,19 @@ def one(T, n, m, k=200, reps=3):
 
 def main():
     L = _lib.load()
-    sizes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1024,2048").split(",")]
+    sizes = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1024,2048,4096").split(",")]
     print(json.dumps({"launch_floor_us": launch_floor()}), flush=True)
     for S in sizes:
         n = m = S - 1
         T = lp.dense_tableau("uniform", 0, n, m)
-        for fused, bpc, var in itertools.product((1, 0), (1, 2, 3, 4, 5), (1, 0, 4, 9)):
+        for fused, bpc, var in itertools.product((1, 0), (3, 4, 5), (0, 1, 9)):
             L.smx_tune_fused(fused)
             L.smx_tune_set(var, bpc)
             us, ok = one(T, n, m)
             print(json.dumps({"size": S, "fused": fused, "bpc": bpc, "variant": var,
                               "us_per_pivot": round(us, 2), "valid": ok}), flush=True)
         L.smx_tune_fused(1)
-        L.smx_tune_set(1, 0)
+        L.smx_tune_set(-2, 0)
 
 
 if __name__ == "__main__":
