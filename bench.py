@@ -3,8 +3,10 @@
 Workload (BASELINE.json configs[3], the north-star target config): a 16384 x 16384 dense fp64
 tableau (n = m = 16383; seeded uniform random LP A~U(-1,1), b~U(0.1,1), c~U(-1,1), feasible at
 the origin so the trajectory is a long phase-2 run), resident in HBM before timing starts.
-A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): the selection
-kernel (pick_element, :70-141) + the fused update kernel (recalculate_matrix, :143-177).
+A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): ONE kernel,
+k_update<kFused> -- the update of step k (recalculate_matrix, :143-177) whose look-ahead
+workgroups also compute step k+1's selection inputs (pick_element, :70-141).  N = 1 times one
+replay of a pre-captured hipGraph of K such kernels.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size S]
 
@@ -15,7 +17,8 @@ synchronize on both sides of exactly K pivots, max over ranks.  Rank 0 prints ON
 
 roofline: algorithmic bytes of the update kernel = 16 B per tableau element per pivot
 (read + write every element once), divided by that kernel's average duration measured with
-HIP events on the solver stream inside the timed region.  traffic: HBM bytes per launch from
+HIP events on the solver stream inside the timed region (N = 1: events around the graph replay
+/ K, so inter-kernel gaps count as kernel time; N > 1: events around every update kernel).  traffic: HBM bytes per launch from
 the committed rocprofv3 PMC summary (profiles/), FETCH_SIZE doubled per the gfx950 correction.
 cpu_baseline: the numpy restatement of the same pivot (oracle/numpy_oracle.py, bit-identical to
 the reference) on the same tableau, single thread, a bounded number of pivots.
@@ -107,7 +110,6 @@ def cpu_baseline(T, n, m, seconds):
 
 
 def run_single(args):
-    import numpy as np
     import torch
     from simplex_mi355x import _lib, lp
     from simplex_mi355x.device import DeviceTableau
@@ -117,20 +119,28 @@ def run_single(args):
     T = lp.dense_tableau(args.kind, args.seed, n, m)
     dev = DeviceTableau(T, n, m, m, device="cuda:0", log_cap=max(1 << 16, args.warmup + args.steps))
     if args.warmup:
-        dev.run_timed(args.warmup)
+        dev.run(args.warmup, graph=True)
         dev.sync_state()
+    # the timed region replays one pre-captured hipGraph of K chained pivots; HIP events on the
+    # solver stream bracket it, so the kernel average below includes the (tiny) inter-kernel gaps
+    dev.prepare(args.steps)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    upd_ms, dev_ms = dev.run_timed(args.steps)
+    ev0.record(dev.stream)
+    dev.run(args.steps, graph=True)
+    ev1.record(dev.stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    dev_ms = ev0.elapsed_time(ev1)
     ctl = dev.sync_state()
     done = int(ctl["npivots"])
     valid = done == args.warmup + args.steps and not ctl["term"]
     cycle = cycle_report(n, m, dev.read_log(0, done))
     bytes_per_pivot = 16.0 * R * C
     fused = _lib.fused_enabled()   # one k_update<kFused> per pivot, else k_select + k_update
-    avg_upd = float(np.mean(upd_ms)) * 1e-3
+    avg_upd = dev_ms * 1e-3 / args.steps   # s per pivot kernel (prime/publish included)
     achieved = bytes_per_pivot / avg_upd / 1e9
     workload = f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
     traffic = load_traffic(args.traffic, f"{R}x{C}")

@@ -201,6 +201,14 @@ class DeviceTableau:
         self.step += k
         self._pending = True
 
+    def prepare(self, k: int) -> None:
+        """Capture (without running) the k-pivot graph the next ``run(k)`` will replay."""
+        self.settle()
+        p = self.step & 1
+        if (p, k) not in self._graphs:
+            with torch.cuda.stream(self.stream):
+                self._make_graph(p, k)
+
     def run_timed(self, k: int):
         """k chained pivots with HIP events around every update kernel (synchronous).
         Returns (per-update-kernel ms array, device ms of the whole chain)."""
