@@ -203,10 +203,27 @@ int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_
                      const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
                      int64_t log_cap, void* ev_before, void* ev_after, void* stream);
 
+/* The same pivot with the fused look-ahead (no select kernel): smx_shard_fused_begin packs the
+ * header and candidate rows from this step's look-ahead records (parts slot `parity`, written by
+ * smx_shard_fused_prime for the first step of a sequence, by the previous fused finish after
+ * that); smx_shard_fused_finish merges, updates and writes the next step's records.  Before
+ * switching back to the unfused calls, smx_fused_publish(next parity) restores ctl->negb. */
+int smx_shard_fused_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                          smx_part* parts, void* stream);
+int smx_shard_fused_begin(const double* T, const smx_shape* shape, int32_t parity,
+                          const smx_ctl* ctl, const smx_part* parts, double* send, void* stream);
+int smx_shard_fused_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                           const smx_shape* shape, int32_t parity, smx_ctl* ctl, smx_part* parts,
+                           int32_t* log, int64_t log_cap, void* ev_before, void* ev_after,
+                           void* stream);
+int smx_fused_publish(const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                      const smx_part* parts, void* stream);
+
 /* Native RCCL driver (one communicator per rank; the unique id is created on rank 0 and
  * shipped to the others by any bootstrap, e.g. torch.distributed.broadcast_object_list).
- * smx_shard_run = k x {select, pack, ncclAllGather on `stream`, update}: no cross-stream waits,
- * no host synchronisation.  RCCL failures are returned as -1000 - ncclResult_t. */
+ * smx_shard_run = k x {select, pack, ncclAllGather on `stream`, update} -- or, with the fused
+ * chain on (smx_tune_fused), prime + k x {fused pack, ncclAllGather, fused update} + publish:
+ * no cross-stream waits, no host synchronisation.  RCCL failures are returned as -1000 - ncclResult_t. */
 int smx_comm_unique_id(void* id_out /* 128 bytes */);
 int smx_comm_init(void** comm_out, int32_t nranks, const void* id, int32_t rank);
 int smx_comm_destroy(void* comm);

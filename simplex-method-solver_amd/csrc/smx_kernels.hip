@@ -456,30 +456,32 @@ __device__ __forceinline__ int block_min_int(int x, int* s_tmp) {
 }
 
 // Fused chain: the select inputs of the NEXT step, computed by nparts workgroups from T_k and
-// step k's pivot (APPLY) -- or from T_k itself to prime a chain (!APPLY).  Workgroup b covers rows
-// b*NT + tid + q*nparts*NT and writes one record:
+// step k's pivot (APPLY) -- or from T_k itself to prime a chain (!APPLY).  T holds `rows` local
+// constraint rows (global index row0 + i) and the f-row at local index `rows`; r_local is the
+// pivot row's local index or -1 (sharded: another rank's row, prow then points into the receive
+// buffer).  Workgroup b covers local rows b*NT + tid + q*nparts*NT and writes one record:
 //   p1col  first row of its slice whose new "-b" entry is negative (simplex.py:72-76), or NONE
 //   first/first_v, best_*  its ratio-test candidates on the new entering column (:105-141)
 // and workgroup 0 stores the entering column itself (first negative new f-row coefficient,
 // simplex.py:94-98) in ctl->negf[slot].  Nothing is min-ed atomically, so no slot needs a reset.
 template <int NT, bool APPLY>
-__device__ void la_partial(const double* __restrict__ T, int64_t ld, int n, int m, int fscan,
-                           int r, int c, double e, const double* __restrict__ prow,
-                           smx_part* __restrict__ out, int b, int nparts,
-                           smx_ctl* __restrict__ ctl, int slot) {
+__device__ void la_partial(const double* __restrict__ T, int64_t ld, int rows, int m, int fscan,
+                           int row0, int r_local, int c, double e,
+                           const double* __restrict__ prow, smx_part* __restrict__ out, int b,
+                           int nparts, smx_ctl* __restrict__ ctl, int slot) {
     __shared__ int s_tmp[NT / kWave];
     __shared__ int s_b[NT / kWave];
     __shared__ First s_f[NT / kWave];
     __shared__ Cand s_c[NT / kWave];
     const int tid = threadIdx.x;
     auto val = [&](int i, int j, double pci) -> double {
-        if (APPLY) return nv(T, ld, r, c, e, prow, i, j, pci);
+        if (APPLY) return nv(T, ld, r_local, c, e, prow, i, j, pci);
         return T[(int64_t)i * ld + j];
     };
     int nf = SMX_NONE;
-    const double pcf = APPLY ? T[(int64_t)n * ld + c] : 0.0;
+    const double pcf = APPLY ? T[(int64_t)rows * ld + c] : 0.0;
     for (int j = tid; j < fscan; j += NT) {
-        if (val(n, j, pcf) < 0.0) {
+        if (val(rows, j, pcf) < 0.0) {
             nf = j;
             break;
         }
@@ -488,20 +490,21 @@ __device__ void la_partial(const double* __restrict__ T, int64_t ld, int n, int 
     int nb = SMX_NONE;
     First f{SMX_NONE, 0.0};
     Cand bc = cand_none();
-    for (int i = b * NT + tid; i < n; i += nparts * NT) {
+    for (int i = b * NT + tid; i < rows; i += nparts * NT) {
+        const int gi = row0 + i;
         const double pci = APPLY ? T[(int64_t)i * ld + c] : 0.0;
         const double bv = val(i, m, pci);
-        if (bv < 0.0 && i < nb) nb = i;
+        if (bv < 0.0 && gi < nb) nb = gi;
         if (nf != SMX_NONE) {
             const double a = val(i, nf, pci);
             if (a != 0.0) {
                 const double v = bv / a;
-                if (i < f.idx) {
-                    f.idx = i;
+                if (gi < f.idx) {
+                    f.idx = gi;
                     f.v = v;
                 }
                 if (!isnan(v)) {
-                    const Cand x = classify(v, i);
+                    const Cand x = classify(v, gi);
                     if (better(x, bc)) bc = x;
                 }
             }
@@ -612,12 +615,12 @@ __device__ Decision decide_fused(const smx_ctl* __restrict__ ctl,
 
 // Prime a fused chain: the look-ahead records of step `parity` from T itself.
 __global__ __launch_bounds__(kUpdBlock) void k_la_prime(const double* __restrict__ T, int64_t ld,
-                                                        int n, int m, int fscan, int parity,
-                                                        smx_ctl* __restrict__ ctl,
+                                                        int rows, int m, int fscan, int row0,
+                                                        int parity, smx_ctl* __restrict__ ctl,
                                                         smx_part* __restrict__ parts) {
     if (ctl->term) return;
-    la_partial<kUpdBlock, false>(T, ld, n, m, fscan, 0, 0, 1.0, T, parts, blockIdx.x, gridDim.x,
-                                 ctl, parity);
+    la_partial<kUpdBlock, false>(T, ld, rows, m, fscan, row0, -1, 0, 1.0, T, parts, blockIdx.x,
+                                 gridDim.x, ctl, parity);
 }
 
 // End of a fused chain: publish the next step's first-negative-b row into ctl->negb[parity]
@@ -649,7 +652,13 @@ __global__ __launch_bounds__(kWave) void k_publish(const smx_part* __restrict__ 
 //                    : (j == c ? x   : x*e - pr*pc) steps 2 and 4
 //     out = num / e
 // which is exactly the value the reference leaves in new_table[i][j] after steps 1-4.
-enum UpdMode { kSingle = 0, kShard = 1, kForced = 2, kFused = 3 };
+//
+// Modes: kSingle (decision from k_select's partials), kShard (decision merged from the gathered
+// shard headers, nparts = rank count), kForced (given r, c), kFused / kShardFused (as kSingle /
+// kShard, plus look-ahead workgroups [0, nparts) writing the next step's records; in these modes
+// forced_r = 1 when the look-ahead workgroups also sweep, and kShardFused's rank count is
+// forced_c).
+enum UpdMode { kSingle = 0, kShard = 1, kForced = 2, kFused = 3, kShardFused = 4 };
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
@@ -687,9 +696,10 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     // kFused: workgroups [0, nparts) compute the look-ahead records; they join the sweep only
     // when forced_r (= "look-ahead sweeps") is set: tableaux beyond the Infinity Cache, whose
     // stream needs every resident wave's loads in flight (launch_update_mode)
-    const bool la_sweep = (MODE == kFused) && forced_r != 0;
-    const int lab = (MODE == kFused && !la_sweep) ? nparts : 0;
-    const bool la = (MODE == kFused) && (int)blockIdx.x < nparts;
+    constexpr bool LA = MODE == kFused || MODE == kShardFused;
+    const bool la_sweep = LA && forced_r != 0;
+    const int lab = (LA && !la_sweep) ? nparts : 0;
+    const bool la = LA && (int)blockIdx.x < nparts;
     const bool sweeps = !la || la_sweep;
     const int NW = ((int)gridDim.x - lab) * kUpdWaves;
     const int w = sweeps ? ((int)blockIdx.x - lab) * kUpdWaves +
@@ -777,10 +787,11 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         r = __builtin_amdgcn_readfirstlane(s_dec[1]);
         c = __builtin_amdgcn_readfirstlane(s_dec[2]);
         prow = Tin + (int64_t)r * ld;
-    } else {  // kShard: every block merges the P gathered headers itself (nparts = P)
+    } else {  // kShard(Fused): every block merges the P gathered headers itself
         __shared__ int64_t s_off;
         if (tid == 0) {
-            const ShardDecision d = merge_headers(recv, nparts, ld, m, flen);
+            const int nranks = (MODE == kShardFused) ? forced_c : nparts;
+            const ShardDecision d = merge_headers(recv, nranks, ld, m, flen);
             s_dec[0] = d.status;
             s_dec[1] = d.r;
             s_dec[2] = d.c;
@@ -797,13 +808,6 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     // history: rows whose new "-b" entry is x1 / x2 of the new tableau (find_optimum)
     int hx0 = -1, hx1 = -1;
     int64_t hslot = 0;
-    if (MODE == kFused && la) {
-        // this workgroup's share of step k+1's select inputs (one kernel per pivot)
-        la_partial<kUpdBlock, true>(Tin, ld, n, m, fscan, r, c, e, prow,
-                                    const_cast<smx_part*>(parts) + (size_t)(parity ^ 1) * nparts,
-                                    blockIdx.x, nparts, ctl, parity ^ 1);
-        if (!la_sweep) return;
-    }
     if ((MODE == kSingle || MODE == kFused) && xhist != nullptr && log_cap > 0) {
         hx0 = move_label(ctl->xpos[parity][0], r, c);
         hx1 = move_label(ctl->xpos[parity][1], r, c);
@@ -812,6 +816,13 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     // local index of the pivot row, -1 when another rank owns it (never the f-row replica,
     // whose local index rows_local may equal r - row0 for a row of the next rank)
     const int r_local = (r >= row0 && r < row0 + rows_local) ? r - row0 : -1;
+    if (LA && la) {
+        // this workgroup's share of step k+1's select inputs (one kernel per pivot)
+        la_partial<kUpdBlock, true>(Tin, ld, rows_local, m, fscan, row0, r_local, c, e, prow,
+                                    const_cast<smx_part*>(parts) + (size_t)(parity ^ 1) * nparts,
+                                    blockIdx.x, nparts, ctl, parity ^ 1);
+        if (!la_sweep) return;
+    }
     int ch_pr = -1;
     dbl2 pr = dbl2{0.0, 0.0};
     const int negslot = parity ^ 1;
@@ -855,7 +866,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
                         if (i == hx0) xhist[hslot] = o[h];
                         if (i == hx1) xhist[hslot + 1] = o[h];
                     }
-                    if (MODE == kFused) {
+                    if (LA) {
                         // next-step scans come from the look-ahead records
                     } else if (i < rows_local) {
                         if (jj == m && o[h] < 0.0) lb = min(lb, row0 + i);
@@ -896,6 +907,9 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
 //   hdr[3] best class, hdr[4] best row (global), hdr[5] best v -> row B = best row (phase 2)
 //   hdr[6] entering column c (replicated f-row => same on every rank)
 //   hdr[7] phase 1: first column j < m with row B [j] > 0 (computed by the row's owner), or NONE
+// FUSED: `parts` are the look-ahead records of this step (p1col = local first-negative-b row,
+// global index); the rank owning that row scans it for the phase-1 column in block 0.
+template <bool FUSED>
 __global__ __launch_bounds__(kUpdBlock) void k_pack(const double* __restrict__ T, int64_t ld,
                                                      int rows, int m, int row0, int parity,
                                                      const smx_ctl* __restrict__ ctl,
@@ -904,15 +918,40 @@ __global__ __launch_bounds__(kUpdBlock) void k_pack(const double* __restrict__ T
     __shared__ int s_rows[2];
     __shared__ int s_hdr_i[4];
     __shared__ double s_hdr_d[2];
+    __shared__ int s_negb;
+    __shared__ int s_tmp[kUpdBlock / kWave];
     const int tid = threadIdx.x;
     if (ctl->term) return;
+    int p1f = SMX_NONE;
+    if (FUSED) {
+        if (tid < kWave) {
+            int nb = SMX_NONE;
+            for (int k = tid; k < nparts; k += kWave) nb = min(nb, parts[k].p1col);
+            nb = wave_min_int(nb);
+            if (tid == 0) s_negb = nb;
+        }
+        __syncthreads();
+        const int nb = s_negb;
+        if (blockIdx.x == 0 && nb != SMX_NONE) {   // simplex.py:81-85 on the owner's row
+            const double* rowp = T + (int64_t)(nb - row0) * ld;
+            for (int j = tid; j < m; j += kUpdBlock) {
+                if (rowp[j] > 0.0) {
+                    p1f = j;
+                    break;
+                }
+            }
+            p1f = block_min_int<kUpdBlock>(p1f, s_tmp);
+        }
+    }
     if (tid < kWave) {
-        const int negb = ctl->negb[parity];
+        const int negb = FUSED ? s_negb : ctl->negb[parity];
         const int c = ctl->negf[parity];
         First f{SMX_NONE, 0.0};
         Cand b = cand_none();
         int p1 = SMX_NONE;   // phase 1: first column with T[negb][j] > 0 (simplex.py:81-85)
-        if (negb != SMX_NONE) {
+        if (FUSED) {
+            p1 = p1f;
+        } else if (negb != SMX_NONE) {
             for (int k = tid; k < nparts; k += kWave) p1 = min(p1, parts[k].p1col);
             p1 = wave_min_int(p1);
         }
@@ -1136,12 +1175,23 @@ int launch_select(const double* T, const smx_shape& s, int parity, smx_ctl* ctl,
     return (int)hipGetLastError();
 }
 
+template <bool FUSED>
+int launch_pack(const double* T, const smx_shape& s, int parity, const smx_ctl* ctl,
+                const smx_part* parts, double* send, hipStream_t st) {
+    int blocks = (int)((s.m + 2 + kUpdBlock - 1) / kUpdBlock);
+    if (blocks > 64) blocks = 64;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_pack<FUSED>, dim3(blocks), dim3(kUpdBlock), 0, st, T, s.ld, s.rows, s.m,
+                       s.row0, parity, ctl, parts, s.nparts, send);
+    return (int)hipGetLastError();
+}
+
 // Fused chain helpers: prime the look-ahead records of step `parity` from T; publish at the end.
 int launch_prime(const double* T, const smx_shape& s, int parity, smx_ctl* ctl, smx_part* parts,
                  hipStream_t st) {
     const int fscan = s.flen < s.m ? s.flen : s.m;
-    hipLaunchKernelGGL(k_la_prime, dim3(s.nparts), dim3(kUpdBlock), 0, st, T, s.ld, s.n, s.m,
-                       fscan, parity, ctl, parts + (size_t)parity * s.nparts);
+    hipLaunchKernelGGL(k_la_prime, dim3(s.nparts), dim3(kUpdBlock), 0, st, T, s.ld, s.rows, s.m,
+                       fscan, s.row0, parity, ctl, parts + (size_t)parity * s.nparts);
     return (int)hipGetLastError();
 }
 
@@ -1278,10 +1328,11 @@ int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int 
     // kFused: the first nparts workgroups compute the look-ahead records; within the Infinity
     // Cache they are reserved (their extra round trips would be the critical path), beyond it
     // they sweep too (profiles/r01_sweep_small.jsonl)
-    const bool la_sweep = MODE == kFused && (int64_t)(s.rows + 1) * s.ld * 8 > kLaSweepTable;
-    int grid = update_grid(s, (const void*)fn, MODE == kFused && !la_sweep ? s.nparts : 0);
+    constexpr bool LA = MODE == kFused || MODE == kShardFused;
+    const bool la_sweep = LA && (int64_t)(s.rows + 1) * s.ld * 8 > kLaSweepTable;
+    int grid = update_grid(s, (const void*)fn, LA && !la_sweep ? s.nparts : 0);
     if (grid < s.nparts) grid = s.nparts;
-    if (MODE == kFused) fr = la_sweep ? 1 : 0;
+    if (LA) fr = la_sweep ? 1 : 0;   // kShardFused: fc = rank count (caller)
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, Tin,
                        Tout, s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl,
                        parts, s.nparts, log, xhist, log_cap, recv, fr, fc);
@@ -1519,13 +1570,7 @@ int smx_update_forced(const double* Tin, double* Tout, const smx_shape* shape, i
 int smx_shard_pack(const double* T, const smx_shape* shape, int32_t parity, const smx_ctl* ctl,
                    const smx_part* parts, double* send, void* stream) {
     if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
-    int blocks = (int)((shape->m + 2 + kUpdBlock - 1) / kUpdBlock);
-    if (blocks > 64) blocks = 64;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_pack, dim3(blocks), dim3(kUpdBlock), 0, S(stream), T, shape->ld,
-                       shape->rows, shape->m, shape->row0, parity & 1, ctl, parts,
-                       shape->nparts, send);
-    return (int)hipGetLastError();
+    return launch_pack<false>(T, *shape, parity & 1, ctl, parts, send, S(stream));
 }
 
 int smx_shard_merge(const double* recv, int32_t nranks, const smx_shape* shape,
@@ -1606,6 +1651,32 @@ int smx_comm_destroy(void* comm) {
 }
 
 namespace {
+// Fused sharded chain, per pivot: k_pack<true> (records of step k -> header + candidate rows of
+// the materialised T_k) -> one ncclAllGather -> k_update<kShardFused> (merge, sweep, records of
+// step k+1).  Primed by k_la_prime, closed by k_publish.  e_upd: 2k events around the updates.
+int shard_chain_fused(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
+                      smx_ctl* ctl, smx_part* parts, double* send, double* recv, int nranks,
+                      ncclComm_t comm, int32_t* log, int64_t log_cap, hipEvent_t* e_upd,
+                      hipStream_t st) {
+    int err = launch_prime(parity ? buf1 : buf0, s, parity, ctl, parts, st);
+    const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)s.ld;
+    for (int step = 0; step < k && !err; ++step) {
+        const int p = (parity + step) & 1;
+        double* tin = p ? buf1 : buf0;
+        double* tout = p ? buf0 : buf1;
+        err = launch_pack<true>(tin, s, p, ctl, parts + (size_t)p * s.nparts, send, st);
+        if (err) break;
+        err = nccl_err(ncclAllGather(send, recv, slot, ncclFloat64, comm, st));
+        if (err) break;
+        if (e_upd) (void)hipEventRecord(e_upd[2 * step], st);
+        err = launch_update_mode<kShardFused>(tin, tout, s, p, ctl, parts, log, nullptr, log_cap,
+                                              recv, 0, nranks, st);
+        if (e_upd) (void)hipEventRecord(e_upd[2 * step + 1], st);
+    }
+    if (!err) err = launch_publish(s, (parity + k) & 1, ctl, parts, st);
+    return err;
+}
+
 int shard_pivot(double* tin, double* tout, const smx_shape& s, int p, smx_ctl* ctl,
                 smx_part* parts, double* send, double* recv, int nranks, ncclComm_t comm,
                 int32_t* log, int64_t log_cap, hipEvent_t e0, hipEvent_t e1, hipStream_t st) {
@@ -1627,6 +1698,10 @@ int smx_shard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
                   smx_ctl* ctl, smx_part* parts, double* send, double* recv, int32_t nranks,
                   void* comm, int32_t* log, int64_t log_cap, void* stream) {
     if (!shape_ok(shape) || !comm || nranks < 1 || k < 0) return (int)hipErrorInvalidValue;
+    if (g_fused && k > 0)
+        return shard_chain_fused(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
+                                 nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap,
+                                 nullptr, S(stream));
     for (int step = 0; step < k; ++step) {
         const int p = (parity + step) & 1;
         const int err = shard_pivot(p ? buf1 : buf0, p ? buf0 : buf1, *shape, p, ctl, parts,
@@ -1654,7 +1729,10 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     }
     (void)hipEventRecord(ev[2 * k], st);
     int err = 0;
-    for (int step = 0; step < k && !err; ++step) {
+    if (g_fused)
+        err = shard_chain_fused(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
+                                nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap, ev, st);
+    for (int step = 0; step < k && !err && !g_fused; ++step) {
         const int p = (parity + step) & 1;
         err = shard_pivot(p ? buf1 : buf0, p ? buf0 : buf1, *shape, p, ctl, parts, send, recv,
                           nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap, ev[2 * step],
@@ -1669,6 +1747,38 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     for (int i = 0; i < 2 * k + 1; ++i) (void)hipEventDestroy(ev[i]);
     delete[] ev;
     return err;
+}
+
+int smx_shard_fused_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                          smx_part* parts, void* stream) {
+    if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
+    return launch_prime(T, *shape, parity & 1, ctl, parts, S(stream));
+}
+
+int smx_shard_fused_begin(const double* T, const smx_shape* shape, int32_t parity,
+                          const smx_ctl* ctl, const smx_part* parts, double* send, void* stream) {
+    if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
+    return launch_pack<true>(T, *shape, parity & 1, ctl,
+                             parts + (size_t)(parity & 1) * shape->nparts, send, S(stream));
+}
+
+int smx_shard_fused_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                           const smx_shape* shape, int32_t parity, smx_ctl* ctl, smx_part* parts,
+                           int32_t* log, int64_t log_cap, void* ev_before, void* ev_after,
+                           void* stream) {
+    if (!shape_ok(shape) || Tin == Tout || nranks < 1) return (int)hipErrorInvalidValue;
+    if (ev_before) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_before), S(stream));
+    const int err = launch_update_mode<kShardFused>(Tin, Tout, *shape, parity & 1, ctl, parts,
+                                                    log, nullptr, log_cap, recv, 0, nranks,
+                                                    S(stream));
+    if (ev_after) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_after), S(stream));
+    return err;
+}
+
+int smx_fused_publish(const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                      const smx_part* parts, void* stream) {
+    if (!shape_ok(shape)) return (int)hipErrorInvalidValue;
+    return launch_publish(*shape, parity & 1, ctl, parts, S(stream));
 }
 
 int smx_shard_begin(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,

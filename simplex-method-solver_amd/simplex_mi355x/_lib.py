@@ -47,7 +47,8 @@ EXPORTS = (
     "smx_run", "smx_run_timed", "smx_graph_create", "smx_graph_launch", "smx_graph_destroy", "smx_update_forced",
     "smx_batch_solve", "smx_comm_unique_id", "smx_comm_init", "smx_comm_destroy",
     "smx_shard_run", "smx_shard_run_timed", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
-    "smx_shard_finish",
+    "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
+    "smx_shard_fused_finish", "smx_fused_publish",
 )
 
 
@@ -100,6 +101,11 @@ def load():
                             ctypes.c_int),
         "smx_shard_begin": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp, vp, vp], ctypes.c_int),
+        "smx_shard_fused_prime": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),
+        "smx_shard_fused_begin": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
+        "smx_shard_fused_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, vp, i64, vp, vp, vp],
+                                   ctypes.c_int),
+        "smx_fused_publish": ([sp, i32, vp, vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -7,7 +7,8 @@ Layout in HBM (one object per tableau, owned by torch tensors):
   ``R = rows + 1`` (constraint rows, then the f-row), ``C = m + 1`` used columns, ``ld`` = C
   rounded up to an even count and to 16 doubles (128-B rows, 16-B ``double2`` lanes).
 * ``ctl``   : 128-B ``struct smx_ctl`` (first-negative slots, selection, pivot counter).
-* ``parts`` : ``nparts`` x 32-B ``struct smx_part`` select partials.
+* ``parts`` : 2 x ``nparts`` 32-B ``struct smx_part`` records (select partials; the fused
+  chain's look-ahead records, double-buffered by parity).
 * ``log``   : ``int32[log_cap][2]`` ring of applied pivots ``(r, c)``, drained by the host.
 * ``xhist`` : ``float64[log_cap][2]`` ring of ``(x1, x2)`` of the tableau after each pivot
   (find_optimum, simplex.py:51-68), written by the update kernel itself.

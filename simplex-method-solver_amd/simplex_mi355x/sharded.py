@@ -65,10 +65,14 @@ class RcclComm:
 
 
 class HipShardBackend:
-    """This rank's slice of the tableau in HBM plus the exchange buffers."""
+    """This rank's slice of the tableau in HBM plus the exchange buffers.
+
+    ``fused`` (default: the library's chain mode, smx_tune_fused): a pivot is fused pack ->
+    all-gather -> fused update, with the next step's look-ahead records written by the update
+    (no select kernel); otherwise select + pack -> all-gather -> update."""
 
     def __init__(self, local_T: np.ndarray, n: int, m: int, flen: int, row0: int, world: int,
-                 device=None, log_cap: int = 1 << 16):
+                 device=None, log_cap: int = 1 << 16, fused: bool | None = None):
         self.dev = DeviceTableau(local_T, n, m, flen, device=device, row0=row0, n_global=n,
                                  log_cap=log_cap)
         self.world = world
@@ -77,13 +81,28 @@ class HipShardBackend:
             self.send = torch.zeros(self.slot, dtype=torch.float64, device=self.dev.device)
             self.recv = torch.zeros(world * self.slot, dtype=torch.float64, device=self.dev.device)
         self._shape = ops.make_shape(self.dev.shape)
+        self.fused = _lib.fused_enabled() if fused is None else bool(fused)
+        self._records = False   # look-ahead records of step dev.step are in dev.parts
 
     def stream_ctx(self):
         return torch.cuda.stream(self.dev.stream)
 
     def begin(self) -> None:
         d = self.dev
-        _lib.check(_lib.load().smx_shard_begin(
+        L = _lib.load()
+        if self.fused:
+            p = d.step & 1
+            if not self._records:
+                _lib.check(L.smx_shard_fused_prime(
+                    d.buf[p].data_ptr(), ctypes.byref(self._shape), p, d.ctl.data_ptr(),
+                    d.parts.data_ptr(), d.stream.cuda_stream), "smx_shard_fused_prime")
+                self._records = True
+            _lib.check(L.smx_shard_fused_begin(
+                d.buf[p].data_ptr(), ctypes.byref(self._shape), p, d.ctl.data_ptr(),
+                d.parts.data_ptr(), self.send.data_ptr(), d.stream.cuda_stream),
+                "smx_shard_fused_begin")
+            return
+        _lib.check(L.smx_shard_begin(
             d.buf[d.step & 1].data_ptr(), ctypes.byref(self._shape), d.step & 1,
             d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(), d.stream.cuda_stream),
             "smx_shard_begin")
@@ -91,6 +110,17 @@ class HipShardBackend:
     def finish(self, ev_before=None, ev_after=None) -> None:
         d = self.dev
         p = d.step & 1
+        if self.fused:
+            _lib.check(_lib.load().smx_shard_fused_finish(
+                d.buf[p].data_ptr(), d.buf[p ^ 1].data_ptr(), self.recv.data_ptr(), self.world,
+                ctypes.byref(self._shape), p, d.ctl.data_ptr(), d.parts.data_ptr(),
+                d.log.data_ptr(), d.log_cap,
+                ev_before.cuda_event if ev_before is not None else None,
+                ev_after.cuda_event if ev_after is not None else None, d.stream.cuda_stream),
+                "smx_shard_fused_finish")
+            d.step += 1
+            d._pending = True
+            return
         _lib.check(_lib.load().smx_shard_finish(
             d.buf[p].data_ptr(), d.buf[p ^ 1].data_ptr(), self.recv.data_ptr(), self.world,
             ctypes.byref(self._shape), p, d.ctl.data_ptr(), d.log.data_ptr(), d.log_cap,
@@ -100,29 +130,45 @@ class HipShardBackend:
         d.step += 1
         d._pending = True
 
+    def _chain_mode(self):
+        """Run the native chain in this backend's mode (smx_tune_fused is process-wide)."""
+        L = _lib.load()
+        prev = L.smx_tune_fused(int(self.fused))
+        return L, prev
+
     def run_native(self, k: int, comm: "RcclComm") -> None:
         """k pivots, all-gathers issued by libsmx.so on the solver stream (no host sync)."""
         d = self.dev
-        _lib.check(_lib.load().smx_shard_run(
-            d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
-            d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(), self.recv.data_ptr(),
-            self.world, comm.handle, d.log.data_ptr(), d.log_cap, d.stream.cuda_stream),
-            "smx_shard_run")
+        L, prev = self._chain_mode()
+        try:
+            _lib.check(L.smx_shard_run(
+                d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1,
+                k, d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(),
+                self.recv.data_ptr(), self.world, comm.handle, d.log.data_ptr(), d.log_cap,
+                d.stream.cuda_stream), "smx_shard_run")
+        finally:
+            L.smx_tune_fused(prev)
         d.step += k
         d._pending = True
+        self._records = self.fused
 
     def run_native_timed(self, k: int, comm: "RcclComm"):
         """Like run_native, with HIP events around every update kernel (synchronous)."""
         d = self.dev
         upd = (ctypes.c_float * k)()
         tot = ctypes.c_float()
-        _lib.check(_lib.load().smx_shard_run_timed(
-            d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
-            d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(), self.recv.data_ptr(),
-            self.world, comm.handle, d.log.data_ptr(), d.log_cap, d.stream.cuda_stream, upd,
-            ctypes.byref(tot)), "smx_shard_run_timed")
+        L, prev = self._chain_mode()
+        try:
+            _lib.check(L.smx_shard_run_timed(
+                d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1,
+                k, d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(),
+                self.recv.data_ptr(), self.world, comm.handle, d.log.data_ptr(), d.log_cap,
+                d.stream.cuda_stream, upd, ctypes.byref(tot)), "smx_shard_run_timed")
+        finally:
+            L.smx_tune_fused(prev)
         d.step += k
         d._pending = True
+        self._records = self.fused
         return np.frombuffer(upd, dtype=np.float32).copy(), float(tot.value)
 
     def state(self) -> dict:
@@ -248,12 +294,13 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
             "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
                        "parallelism": f"row-shard x{world} (1 RCCL all-gather per pivot, "
                                       "issued natively on the solver stream)",
-                       "rows_per_rank": hi - lo, "kernels_per_pivot": 3,
+                       "rows_per_rank": hi - lo, "kernels_per_pivot": 2 if be.fused else 3,
                        "collectives_per_pivot": 1},
             "hbm_gbs_per_pivot": 16.0 * R * C / (wall / args.steps) / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak_gbs, "unit": "GB/s",
                          "frac": achieved / peak_gbs, "traffic": traffic,
-                         "kernel": "k_update<kShard> (rank 0)",
+                         "kernel": ("k_update<kShardFused>" if be.fused else "k_update<kShard>")
+                                   + " (rank 0)",
                          "algorithmic_bytes_per_launch": local_bytes,
                          "avg_kernel_ms": avg_upd * 1e3,
                          "max_rank_avg_kernel_ms": float(mx[1])},

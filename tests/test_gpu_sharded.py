@@ -1,6 +1,6 @@
-"""GPU: the HIP shard kernels (k_select/k_pack/k_merge/k_update<kShard>) for P simulated ranks in
-one process on one device (the all-gather done by a device copy), against the unsharded C oracle,
-bit for bit.  The multi-process RCCL path itself is covered by bench.py --sharded (world 1 on the
+"""GPU: the HIP shard kernels for P simulated ranks in one process on one device (the all-gather
+done by a device copy), against the unsharded C oracle, bit for bit -- both pivot forms: unfused
+(k_select/k_pack/k_update<kShard>) and fused (k_la_prime/k_pack<fused>/k_update<kShardFused>).  The multi-process RCCL path itself is covered by bench.py --sharded (world 1 on the
 test box) and by the gloo tests of the same driver."""
 from __future__ import annotations
 
@@ -17,14 +17,15 @@ def _need_gpu():
         pytest.skip("needs an MI355X")
 
 
-def _simulate(T, n, m, k, P):
+def _simulate(T, n, m, k, P, fused=True, bes=None):
     import torch
     from simplex_mi355x.sharded import HipShardBackend, row_range
-    bes = []
-    for p in range(P):
-        lo, hi = row_range(n, p, P)
-        local = np.concatenate([T[lo:hi], T[n:n + 1]], axis=0)
-        bes.append(HipShardBackend(local, n, m, m, lo, P))
+    if bes is None:
+        bes = []
+        for p in range(P):
+            lo, hi = row_range(n, p, P)
+            local = np.concatenate([T[lo:hi], T[n:n + 1]], axis=0)
+            bes.append(HipShardBackend(local, n, m, m, lo, P, fused=fused))
     for _ in range(k):
         for be in bes:
             with be.stream_ctx():
@@ -42,9 +43,10 @@ def _simulate(T, n, m, k, P):
     logs = [be.log(0, s["npivots"]) for be, s in zip(bes, states)]
     tables = [be.local_table() for be in bes]
     full = np.concatenate([t[:-1] for t in tables] + [tables[0][-1:]], axis=0)
-    return states, logs, tables, full
+    return states, logs, tables, full, bes
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("kind,n,m,k,P", [
     ("uniform", 1023, 1023, 80, 2),
     ("uniform", 1001, 777, 80, 3),
@@ -55,11 +57,11 @@ def _simulate(T, n, m, k, P):
     ("uniform", 40, 30, 78, 3),   # step 26 pivots on row 26 = rank 2's first row: on rank 1
                                   # r - row0 == its f-row replica's local index (regression)
 ])
-def test_hip_shards_match_oracle(kind, n, m, k, P):
+def test_hip_shards_match_oracle(kind, n, m, k, P, fused):
     from oracle import c_oracle
     from simplex_mi355x import lp
     T = lp.dense_tableau(kind, 7, n, m)
-    states, logs, tables, full = _simulate(T, n, m, k, P)
+    states, logs, tables, full, _ = _simulate(T, n, m, k, P, fused)
     Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
     for s, lg in zip(states, logs):
         assert s["npivots"] == done
@@ -70,13 +72,14 @@ def test_hip_shards_match_oracle(kind, n, m, k, P):
     assert np.array_equal(full[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
 
 
-def test_hip_shards_terminal_outcome():
+@pytest.mark.parametrize("fused", [True, False])
+def test_hip_shards_terminal_outcome(fused):
     """A run that ends (optimum or error) stops identically on every rank."""
     from oracle import c_oracle
     from simplex_mi355x import lp
     n, m = 40, 30
     T = lp.dense_tableau("uniform", 2, n, m)
-    states, logs, tables, full = _simulate(T, n, m, 400, 3)
+    states, logs, tables, full, _ = _simulate(T, n, m, 400, 3, fused)
     Tref, st, done, log = c_oracle.run(T, n, m, m, 400)
     assert done < 400
     for s in states:
@@ -93,3 +96,27 @@ def test_native_rccl_driver_world1():
     out = subprocess.run([sys.executable, os.path.join(repo, "tools", "check_native_shard.py")],
                          capture_output=True, text=True, timeout=600, cwd=repo)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+
+
+def test_hip_shards_fused_then_unfused():
+    """Fused steps, smx_fused_publish, then unfused steps continue the same trajectory."""
+    import ctypes
+    import torch
+    from oracle import c_oracle
+    from simplex_mi355x import _lib, lp
+    n, m, P = 600, 500, 3
+    T = lp.dense_tableau("mixed", 11, n, m)
+    _, _, _, _, bes = _simulate(T, n, m, 37, P, fused=True)
+    L = _lib.load()
+    for be in bes:
+        d = be.dev
+        _lib.check(L.smx_fused_publish(ctypes.byref(be._shape), d.step & 1, d.ctl.data_ptr(),
+                                       d.parts.data_ptr(), d.stream.cuda_stream), "publish")
+        be.fused = False
+    torch.cuda.synchronize()
+    states, logs, tables, full, _ = _simulate(T, n, m, 45, P, bes=bes)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, 82, threads=8)
+    for s_, lg in zip(states, logs):
+        assert s_["npivots"] == done
+        assert np.array_equal(lg, log)
+    assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))
