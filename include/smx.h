@@ -118,7 +118,8 @@ int smx_set_xpos(smx_ctl* ctl, int32_t parity, int32_t x1code, int32_t x2code, v
 int smx_select(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                smx_part* parts, void* stream);
 
-/* Fused chain (default for smx_run / smx_run_timed / smx_graph_*): ONE kernel per pivot --
+/* Fused chain (default for smx_run / smx_run_timed / smx_graph_*; `on`: 0 off, 1 on, 2 on plus
+ * the overlapped form of smx_shard_run): ONE kernel per pivot --
  * the update of step k, whose first nparts workgroups also compute step k+1's select inputs
  * (first negative new "-b" row, entering column, ratio-test partials) from T_k with the update's
  * own arithmetic (bit-identical); a chain is primed by one small kernel and ends with a one-wave
@@ -218,12 +219,26 @@ int smx_shard_fused_finish(const double* Tin, double* Tout, const double* recv, 
                            void* stream);
 int smx_fused_publish(const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                       const smx_part* parts, void* stream);
+/* The two halves of a step of the overlapped chain (smx_shard_run's default form), for callers
+ * that drive the exchange themselves: after step k's all-gather into `recv`,
+ * smx_shard_ahead computes step k+1's records (parts slot parity^1) and packs step k+1's header
+ * and candidate rows into `send` from T_k (it may run concurrently with the sweep, on another
+ * stream); smx_shard_sweep is step k's update.  Start a sequence with smx_shard_fused_prime +
+ * smx_shard_fused_begin. */
+int smx_shard_ahead(const double* T, const smx_shape* shape, int32_t parity, const double* recv,
+                    int32_t nranks, smx_ctl* ctl, smx_part* parts, double* send, void* stream);
+int smx_shard_sweep(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                    const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
+                    int64_t log_cap, void* stream);
 
 /* Native RCCL driver (one communicator per rank; the unique id is created on rank 0 and
  * shipped to the others by any bootstrap, e.g. torch.distributed.broadcast_object_list).
- * smx_shard_run = k x {select, pack, ncclAllGather on `stream`, update} -- or, with the fused
- * chain on (smx_tune_fused), prime + k x {fused pack, ncclAllGather, fused update} + publish:
- * no cross-stream waits, no host synchronisation.  RCCL failures are returned as -1000 - ncclResult_t. */
+ * smx_shard_run = k x {select, pack, ncclAllGather on `stream`, update}; with smx_tune_fused(1)
+ * (the default) prime + k x {fused pack, ncclAllGather, fused update} + publish; with
+ * smx_tune_fused(2) the overlapped form: the update sweeps on `stream` while an internal exchange
+ * stream computes the next step's look-ahead records, header and candidate rows from T_k and
+ * gathers them (two events per step).  No host synchronisation.  `recv` must hold
+ * 2 * nranks * (SMX_SHARD_HDR + 2 * ld) doubles (the second half is used by the overlapped form).  RCCL failures are returned as -1000 - ncclResult_t. */
 int smx_comm_unique_id(void* id_out /* 128 bytes */);
 int smx_comm_init(void** comm_out, int32_t nranks, const void* id, int32_t rank);
 int smx_comm_destroy(void* comm);

@@ -1012,6 +1012,131 @@ __global__ __launch_bounds__(kWave) void k_merge(const double* __restrict__ recv
 
 
 // ---------------------------------------------------------------------------------------------
+// Overlapped sharded chain (smx_shard_run with the fused chain on): while k_update<kShardFused>
+// sweeps T_k -> T_{k+1} on the solver stream, the exchange stream computes step k+1's records
+// (k_shard_la) and header + candidate rows (k_pack_ahead) from T_k and step k's gathered pivot
+// row with the update's own expression (nv), then all-gathers them -- so the collective runs
+// under the sweep.  Both kernels re-derive step k's decision from the gathered headers
+// (merge_headers is a pure function of recv) and do nothing when it is terminal.
+__device__ __forceinline__ bool merged_pivot(const double* __restrict__ recv, int nranks,
+                                             int64_t ld, int m, int flen, int* s_dec,
+                                             int64_t* s_off) {
+    if (threadIdx.x == 0) {
+        const ShardDecision d = merge_headers(recv, nranks, ld, m, flen);
+        s_dec[0] = d.status;
+        s_dec[1] = d.r;
+        s_dec[2] = d.c;
+        *s_off = d.off;
+    }
+    __syncthreads();
+    return s_dec[0] == SMX_PIVOT;
+}
+
+__global__ __launch_bounds__(kUpdBlock) void k_shard_la(const double* __restrict__ T, int64_t ld,
+                                                        int rows, int m, int flen, int fscan,
+                                                        int row0, const double* __restrict__ recv,
+                                                        int nranks, smx_ctl* __restrict__ ctl,
+                                                        smx_part* __restrict__ out, int slot) {
+    __shared__ int s_dec[3];
+    __shared__ int64_t s_off;
+    if (ctl->term) return;
+    if (!merged_pivot(recv, nranks, ld, m, flen, s_dec, &s_off)) return;
+    const int r = s_dec[1], c = s_dec[2];
+    const double* prow = recv + s_off;
+    const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
+    la_partial<kUpdBlock, true>(T, ld, rows, m, fscan, row0, r_local, c, prow[c], prow, out,
+                                blockIdx.x, gridDim.x, ctl, slot);
+}
+
+// Header + candidate rows of step k+1 (layout of k_pack) from step k+1's records (`parts`, slot
+// `slot`) and T_k: every value is nv(T_k, pivot k), i.e. exactly T_{k+1}.
+__global__ __launch_bounds__(kUpdBlock) void k_pack_ahead(
+    const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int row0,
+    const double* __restrict__ recv, int nranks, const smx_ctl* __restrict__ ctl,
+    const smx_part* __restrict__ parts, int nparts, int slot, double* __restrict__ send) {
+    __shared__ int s_dec[3];
+    __shared__ int64_t s_off;
+    __shared__ int s_rows[2];
+    __shared__ int s_hdr_i[4];
+    __shared__ double s_hdr_d[2];
+    __shared__ int s_tmp[kUpdBlock / kWave];
+    const int tid = threadIdx.x;
+    if (ctl->term) return;
+    if (!merged_pivot(recv, nranks, ld, m, flen, s_dec, &s_off)) return;
+    const int r = s_dec[1], c = s_dec[2];
+    const double* prow = recv + s_off;
+    const double e = prow[c];
+    const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
+    const int cn = ctl->negf[slot];   // step k+1's entering column (k_shard_la, block 0)
+    if (tid < kWave) {
+        int nb = SMX_NONE;
+        First f{SMX_NONE, 0.0};
+        Cand b = cand_none();
+        for (int k = tid; k < nparts; k += kWave) {
+            const smx_part p = parts[k];
+            nb = min(nb, p.p1col);
+            if (p.first < f.idx) {
+                f.idx = p.first;
+                f.v = p.first_v;
+            }
+            Cand o{p.best_cls, p.best_i, p.best_v};
+            if (better(o, b)) b = o;
+        }
+        nb = wave_min_int(nb);
+        f = wave_first(f);
+        b = wave_best(b);
+        if (nb != SMX_NONE || cn == SMX_NONE) {   // phase 1 / no entering column: no ratio test
+            f = First{SMX_NONE, 0.0};
+            b = cand_none();
+        }
+        if (tid == 0) {
+            s_rows[0] = (f.idx != SMX_NONE && isnan(f.v)) ? f.idx - row0 : -1;     // row A
+            s_rows[1] = (nb != SMX_NONE) ? nb - row0 : (b.cls < 3 ? b.idx - row0 : -1);
+            s_hdr_i[0] = nb;
+            s_hdr_i[1] = f.idx;
+            s_hdr_i[2] = b.cls;
+            s_hdr_i[3] = b.idx;
+            s_hdr_d[0] = f.v;
+            s_hdr_d[1] = b.v;
+        }
+    }
+    __syncthreads();
+    const int ra = s_rows[0], rb = s_rows[1];
+    const int nb = s_hdr_i[0];
+    if (blockIdx.x == 0) {
+        int p1 = SMX_NONE;   // phase 1 (simplex.py:81-85) on the new values of the owner's row
+        if (nb != SMX_NONE) {
+            const int il = nb - row0;
+            const double pci = T[(int64_t)il * ld + c];
+            for (int j = tid; j < m; j += kUpdBlock) {
+                if (nv(T, ld, r_local, c, e, prow, il, j, pci) > 0.0) {
+                    p1 = j;
+                    break;
+                }
+            }
+            p1 = block_min_int<kUpdBlock>(p1, s_tmp);
+        }
+        if (tid == 0) {
+            send[0] = (double)nb;
+            send[1] = (double)s_hdr_i[1];
+            send[2] = s_hdr_d[0];
+            send[3] = (double)s_hdr_i[2];
+            send[4] = (double)s_hdr_i[3];
+            send[5] = s_hdr_d[1];
+            send[6] = (double)cn;
+            send[7] = (double)p1;
+        }
+    }
+    const int C = m + 1;
+    const double pca = ra >= 0 ? T[(int64_t)ra * ld + c] : 0.0;
+    const double pcb = rb >= 0 ? T[(int64_t)rb * ld + c] : 0.0;
+    for (int j = blockIdx.x * kUpdBlock + tid; j < C; j += gridDim.x * kUpdBlock) {
+        if (ra >= 0) send[SMX_SHARD_HDR + j] = nv(T, ld, r_local, c, e, prow, ra, j, pca);
+        if (rb >= 0) send[SMX_SHARD_HDR + ld + j] = nv(T, ld, r_local, c, e, prow, rb, j, pcb);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_batch: many small LPs, one wavefront each (the UI's workload, m = 2,
 // n = 3..20, main.py:309-313).  Lane i holds row i of its LP in registers (rows 0..n, the
 // f-row is lane n), so the whole get_solution loop (simplex.py:184-198) runs inside one launch:
@@ -1322,7 +1447,8 @@ int update_grid(const smx_shape& s, const void* fn, int reserved) {
 template <int MODE>
 int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int parity,
                        smx_ctl* ctl, const smx_part* parts, int32_t* log, double* xhist,
-                       int64_t log_cap, const double* recv, int fr, int fc, hipStream_t st) {
+                       int64_t log_cap, const double* recv, int fr, int fc, hipStream_t st,
+                       int reserve = 0) {
     const int v = variant_for(s);
     UpdFn fn = upd_fn<MODE>(v);
     // kFused: the first nparts workgroups compute the look-ahead records; within the Infinity
@@ -1330,8 +1456,11 @@ int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int 
     // they sweep too (profiles/r01_sweep_small.jsonl)
     constexpr bool LA = MODE == kFused || MODE == kShardFused;
     const bool la_sweep = LA && (int64_t)(s.rows + 1) * s.ld * 8 > kLaSweepTable;
-    int grid = update_grid(s, (const void*)fn, LA && !la_sweep ? s.nparts : 0);
+    // reserve: resident slots left free for kernels of another stream (overlapped shard chain)
+    int grid = update_grid(s, (const void*)fn, (LA && !la_sweep ? s.nparts : 0) + reserve) -
+               reserve;
     if (grid < s.nparts) grid = s.nparts;
+    if (grid < 1) grid = 1;
     if (LA) fr = la_sweep ? 1 : 0;   // kShardFused: fc = rank count (caller)
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, Tin,
                        Tout, s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl,
@@ -1346,7 +1475,11 @@ int launch_update(const double* Tin, double* Tout, const smx_shape& s, int parit
                                        nullptr, 0, 0, st);
 }
 
-int g_fused = 1;   // one kernel per pivot in chains (smx_tune_fused)
+// Chains (smx_tune_fused): 0 select + update; 1 one fused kernel per pivot (default); 2 as 1, and
+// the sharded chain overlaps the next step's look-ahead + all-gather with the sweep on a second
+// stream -- correct, but slower on this stack: the two cross-stream waits per step cost more than
+// the all-gather they hide (profiles/r01_shard_overlap_trace.txt).
+int g_fused = 1;
 
 int launch_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, smx_ctl* ctl,
                  smx_part* parts, int32_t* log, double* xhist, int64_t log_cap, hipStream_t st) {
@@ -1409,7 +1542,7 @@ int smx_tune_set(int32_t variant, int32_t blocks_per_cu_override) {
 
 int smx_tune_fused(int32_t on) {
     const int prev = g_fused;
-    if (on >= 0) g_fused = on ? 1 : 0;
+    if (on >= 0) g_fused = on > 2 ? 2 : on;
     return prev;
 }
 
@@ -1677,6 +1810,105 @@ int shard_chain_fused(double* buf0, double* buf1, const smx_shape& s, int parity
     return err;
 }
 
+// The two halves of an overlapped sharded step (also exported for the P-rank simulation tests):
+// ahead = step k+1's records (s.nparts of them, slot parity^1) and, if `pack`, its header and
+// candidate rows into `send`, from T_k and step k's gathered headers; sweep = the update of step
+// k without look-ahead workgroups, leaving `reserve` resident slots free.
+int launch_ahead(const double* T, const smx_shape& s, int parity, const double* recv,
+                 int nranks, smx_ctl* ctl, smx_part* parts, double* send, bool pack,
+                 hipStream_t st) {
+    smx_part* pn = parts + (size_t)(parity ^ 1) * s.nparts;
+    hipLaunchKernelGGL(k_shard_la, dim3(s.nparts), dim3(kUpdBlock), 0, st, T, s.ld, s.rows, s.m,
+                       s.flen, fscan_of(s), s.row0, recv, nranks, ctl, pn, parity ^ 1);
+    if (pack)
+        hipLaunchKernelGGL(k_pack_ahead, dim3(s.nparts), dim3(kUpdBlock), 0, st, T, s.ld, s.rows,
+                           s.m, s.flen, s.row0, recv, nranks, ctl, pn, s.nparts, parity ^ 1,
+                           send);
+    return (int)hipGetLastError();
+}
+
+int launch_sweep(const double* Tin, double* Tout, const smx_shape& s, int parity,
+                 const double* recv, int nranks, smx_ctl* ctl, int32_t* log, int64_t log_cap,
+                 int reserve, hipStream_t st) {
+    smx_shape sy = s;
+    sy.nparts = 0;   // no look-ahead workgroups
+    return launch_update_mode<kShardFused>(Tin, Tout, sy, parity, ctl, nullptr, log, nullptr,
+                                           log_cap, recv, 0, nranks, st, reserve);
+}
+
+// The exchange stream and two events of the overlapped chain, created once per device.
+struct Overlap {
+    hipStream_t s2 = nullptr;
+    hipEvent_t ev_sweep = nullptr, ev_gather = nullptr;
+};
+
+int overlap_for_device(Overlap** out) {
+    static Overlap cache[64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
+    Overlap& o = cache[dev];
+    if (!o.s2) {
+        hipError_t e = hipStreamCreateWithFlags(&o.s2, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&o.ev_sweep, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&o.ev_gather, hipEventDisableTiming);
+        if (e != hipSuccess) return (int)e;
+    }
+    *out = &o;
+    return 0;
+}
+
+constexpr int kOverlapParts = 16;   // look-ahead workgroups of the overlapped chain
+
+// Overlapped sharded chain.  recv holds two gather slots (step parity).  Per step k:
+//   S2: wait(T_k ready) -> k_shard_la (records of k+1) -> k_pack_ahead -> all-gather into
+//       recv[(k+1)&1] -> record ev_gather
+//   S1: k_update<kShardFused> without look-ahead workgroups (T_k -> T_{k+1}, pivot from
+//       recv[k&1]) -> wait(ev_gather) -> record ev_sweep
+// S1 waiting for the gather before the next sweep also orders S2's reads of T_k before the
+// sweep that overwrites it.  The last step computes the records of step k (for a continuation)
+// but no pack/gather.
+int shard_chain_overlap(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
+                        smx_ctl* ctl, smx_part* parts, double* send, double* recv, int nranks,
+                        ncclComm_t comm, int32_t* log, int64_t log_cap, hipEvent_t* e_upd,
+                        hipStream_t st) {
+    Overlap* o = nullptr;
+    int err = overlap_for_device(&o);
+    if (err) return err;
+    smx_shape sx = s;
+    sx.nparts = s.nparts < kOverlapParts ? s.nparts : kOverlapParts;
+    const int npx = sx.nparts;
+    const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)s.ld;
+    const size_t rsz = (size_t)nranks * slot;
+    double* T0 = parity ? buf1 : buf0;
+    err = launch_prime(T0, sx, parity, ctl, parts, st);
+    if (!err) err = launch_pack<true>(T0, sx, parity, ctl, parts + (size_t)parity * npx, send, st);
+    if (!err) err = nccl_err(ncclAllGather(send, recv + (size_t)parity * rsz, slot, ncclFloat64,
+                                           comm, st));
+    if (!err) err = (int)hipEventRecord(o->ev_sweep, st);
+    for (int step = 0; step < k && !err; ++step) {
+        const int p = (parity + step) & 1;
+        double* tin = p ? buf1 : buf0;
+        double* tout = p ? buf0 : buf1;
+        const double* rc = recv + (size_t)p * rsz;
+        double* rn = recv + (size_t)(p ^ 1) * rsz;
+        const bool more = step + 1 < k;
+        err = (int)hipStreamWaitEvent(o->s2, o->ev_sweep, 0);
+        if (!err) err = launch_ahead(tin, sx, p, rc, nranks, ctl, parts, send, more, o->s2);
+        if (!err && more)
+            err = nccl_err(ncclAllGather(send, rn, slot, ncclFloat64, comm, o->s2));
+        if (!err) err = (int)hipEventRecord(o->ev_gather, o->s2);
+        if (err) break;
+        if (e_upd) (void)hipEventRecord(e_upd[2 * step], st);
+        err = launch_sweep(tin, tout, s, p, rc, nranks, ctl, log, log_cap, npx, st);
+        if (e_upd) (void)hipEventRecord(e_upd[2 * step + 1], st);
+        if (!err) err = (int)hipStreamWaitEvent(st, o->ev_gather, 0);
+        if (!err) err = (int)hipEventRecord(o->ev_sweep, st);
+    }
+    if (!err) err = launch_publish(sx, (parity + k) & 1, ctl, parts, st);
+    return err;
+}
+
 int shard_pivot(double* tin, double* tout, const smx_shape& s, int p, smx_ctl* ctl,
                 smx_part* parts, double* send, double* recv, int nranks, ncclComm_t comm,
                 int32_t* log, int64_t log_cap, hipEvent_t e0, hipEvent_t e1, hipStream_t st) {
@@ -1698,6 +1930,10 @@ int smx_shard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
                   smx_ctl* ctl, smx_part* parts, double* send, double* recv, int32_t nranks,
                   void* comm, int32_t* log, int64_t log_cap, void* stream) {
     if (!shape_ok(shape) || !comm || nranks < 1 || k < 0) return (int)hipErrorInvalidValue;
+    if (g_fused == 2 && k > 0)
+        return shard_chain_overlap(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
+                                   nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap,
+                                   nullptr, S(stream));
     if (g_fused && k > 0)
         return shard_chain_fused(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
                                  nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap,
@@ -1729,7 +1965,11 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     }
     (void)hipEventRecord(ev[2 * k], st);
     int err = 0;
-    if (g_fused)
+    if (g_fused == 2)
+        err = shard_chain_overlap(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
+                                  nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap, ev,
+                                  st);
+    else if (g_fused)
         err = shard_chain_fused(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
                                 nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap, ev, st);
     for (int step = 0; step < k && !err && !g_fused; ++step) {
@@ -1773,6 +2013,20 @@ int smx_shard_fused_finish(const double* Tin, double* Tout, const double* recv, 
                                                     S(stream));
     if (ev_after) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_after), S(stream));
     return err;
+}
+
+int smx_shard_ahead(const double* T, const smx_shape* shape, int32_t parity, const double* recv,
+                    int32_t nranks, smx_ctl* ctl, smx_part* parts, double* send, void* stream) {
+    if (!shape_ok(shape) || nranks < 1) return (int)hipErrorInvalidValue;
+    return launch_ahead(T, *shape, parity & 1, recv, nranks, ctl, parts, send, true, S(stream));
+}
+
+int smx_shard_sweep(const double* Tin, double* Tout, const double* recv, int32_t nranks,
+                    const smx_shape* shape, int32_t parity, smx_ctl* ctl, int32_t* log,
+                    int64_t log_cap, void* stream) {
+    if (!shape_ok(shape) || Tin == Tout || nranks < 1) return (int)hipErrorInvalidValue;
+    return launch_sweep(Tin, Tout, *shape, parity & 1, recv, nranks, ctl, log, log_cap, 0,
+                        S(stream));
 }
 
 int smx_fused_publish(const smx_shape* shape, int32_t parity, smx_ctl* ctl,

@@ -48,7 +48,7 @@ EXPORTS = (
     "smx_batch_solve", "smx_comm_unique_id", "smx_comm_init", "smx_comm_destroy",
     "smx_shard_run", "smx_shard_run_timed", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
     "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
-    "smx_shard_fused_finish", "smx_fused_publish",
+    "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
 )
 
 
@@ -106,6 +106,8 @@ def load():
         "smx_shard_fused_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, vp, i64, vp, vp, vp],
                                    ctypes.c_int),
         "smx_fused_publish": ([sp, i32, vp, vp, vp], ctypes.c_int),
+        "smx_shard_ahead": ([vp, sp, i32, vp, i32, vp, vp, vp, vp], ctypes.c_int),
+        "smx_shard_sweep": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

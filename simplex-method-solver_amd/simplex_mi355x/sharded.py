@@ -69,20 +69,29 @@ class HipShardBackend:
 
     ``fused`` (default: the library's chain mode, smx_tune_fused): a pivot is fused pack ->
     all-gather -> fused update, with the next step's look-ahead records written by the update
-    (no select kernel); otherwise select + pack -> all-gather -> update."""
+    (no select kernel); otherwise select + pack -> all-gather -> update.  ``overlap`` (fused
+    only, off by default): the native chain (run_native*) runs the next step's look-ahead and
+    all-gather on a second stream under the sweep -- slower on this stack, see DESIGN.md §12."""
 
     def __init__(self, local_T: np.ndarray, n: int, m: int, flen: int, row0: int, world: int,
-                 device=None, log_cap: int = 1 << 16, fused: bool | None = None):
+                 device=None, log_cap: int = 1 << 16, fused: bool | None = None,
+                 overlap: bool = False):
         self.dev = DeviceTableau(local_T, n, m, flen, device=device, row0=row0, n_global=n,
                                  log_cap=log_cap)
         self.world = world
         self.slot = ops.shard_slot(self.dev.ld)
         with torch.cuda.stream(self.dev.stream):
             self.send = torch.zeros(self.slot, dtype=torch.float64, device=self.dev.device)
-            self.recv = torch.zeros(world * self.slot, dtype=torch.float64, device=self.dev.device)
+            # two gather slots: the overlapped native chain alternates them by step parity;
+            # the per-step path (begin / all-gather / finish) uses the first
+            self._recv2 = torch.zeros(2 * world * self.slot, dtype=torch.float64,
+                                      device=self.dev.device)
+            self.recv = self._recv2[:world * self.slot]
         self._shape = ops.make_shape(self.dev.shape)
         self.fused = _lib.fused_enabled() if fused is None else bool(fused)
+        self.overlap = bool(overlap) and self.fused
         self._records = False   # look-ahead records of step dev.step are in dev.parts
+        self._packed = False    # overlap form: send already holds step dev.step's pack
 
     def stream_ctx(self):
         return torch.cuda.stream(self.dev.stream)
@@ -92,6 +101,8 @@ class HipShardBackend:
         L = _lib.load()
         if self.fused:
             p = d.step & 1
+            if self.overlap and self._packed:
+                return          # packed by the previous finish (smx_shard_ahead)
             if not self._records:
                 _lib.check(L.smx_shard_fused_prime(
                     d.buf[p].data_ptr(), ctypes.byref(self._shape), p, d.ctl.data_ptr(),
@@ -110,6 +121,26 @@ class HipShardBackend:
     def finish(self, ev_before=None, ev_after=None) -> None:
         d = self.dev
         p = d.step & 1
+        if self.overlap:
+            L = _lib.load()
+            # step k+1's records + pack from T_k (the native chain runs this on its exchange
+            # stream, concurrently with the sweep), then step k's sweep
+            _lib.check(L.smx_shard_ahead(
+                d.buf[p].data_ptr(), ctypes.byref(self._shape), p, self.recv.data_ptr(),
+                self.world, d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(),
+                d.stream.cuda_stream), "smx_shard_ahead")
+            if ev_before is not None:
+                ev_before.record(d.stream)
+            _lib.check(L.smx_shard_sweep(
+                d.buf[p].data_ptr(), d.buf[p ^ 1].data_ptr(), self.recv.data_ptr(), self.world,
+                ctypes.byref(self._shape), p, d.ctl.data_ptr(), d.log.data_ptr(), d.log_cap,
+                d.stream.cuda_stream), "smx_shard_sweep")
+            if ev_after is not None:
+                ev_after.record(d.stream)
+            self._packed = True
+            d.step += 1
+            d._pending = True
+            return
         if self.fused:
             _lib.check(_lib.load().smx_shard_fused_finish(
                 d.buf[p].data_ptr(), d.buf[p ^ 1].data_ptr(), self.recv.data_ptr(), self.world,
@@ -133,7 +164,7 @@ class HipShardBackend:
     def _chain_mode(self):
         """Run the native chain in this backend's mode (smx_tune_fused is process-wide)."""
         L = _lib.load()
-        prev = L.smx_tune_fused(int(self.fused))
+        prev = L.smx_tune_fused((2 if self.overlap else 1) if self.fused else 0)
         return L, prev
 
     def run_native(self, k: int, comm: "RcclComm") -> None:
@@ -144,13 +175,13 @@ class HipShardBackend:
             _lib.check(L.smx_shard_run(
                 d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1,
                 k, d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(),
-                self.recv.data_ptr(), self.world, comm.handle, d.log.data_ptr(), d.log_cap,
+                self._recv2.data_ptr(), self.world, comm.handle, d.log.data_ptr(), d.log_cap,
                 d.stream.cuda_stream), "smx_shard_run")
         finally:
             L.smx_tune_fused(prev)
         d.step += k
         d._pending = True
-        self._records = self.fused
+        self._records = self._packed = False   # the native chain may keep fewer records
 
     def run_native_timed(self, k: int, comm: "RcclComm"):
         """Like run_native, with HIP events around every update kernel (synchronous)."""
@@ -162,13 +193,13 @@ class HipShardBackend:
             _lib.check(L.smx_shard_run_timed(
                 d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1,
                 k, d.ctl.data_ptr(), d.parts.data_ptr(), self.send.data_ptr(),
-                self.recv.data_ptr(), self.world, comm.handle, d.log.data_ptr(), d.log_cap,
+                self._recv2.data_ptr(), self.world, comm.handle, d.log.data_ptr(), d.log_cap,
                 d.stream.cuda_stream, upd, ctypes.byref(tot)), "smx_shard_run_timed")
         finally:
             L.smx_tune_fused(prev)
         d.step += k
         d._pending = True
-        self._records = self.fused
+        self._records = self._packed = False
         return np.frombuffer(upd, dtype=np.float32).copy(), float(tot.value)
 
     def state(self) -> dict:
@@ -295,6 +326,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
                        "parallelism": f"row-shard x{world} (1 RCCL all-gather per pivot, "
                                       "issued natively on the solver stream)",
                        "rows_per_rank": hi - lo, "kernels_per_pivot": 2 if be.fused else 3,
+                       "gather_overlapped_with_sweep": be.overlap,
                        "collectives_per_pivot": 1},
             "hbm_gbs_per_pivot": 16.0 * R * C / (wall / args.steps) / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak_gbs, "unit": "GB/s",

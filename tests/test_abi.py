@@ -94,3 +94,24 @@ def test_lp_generator_is_shardable():
     assert np.array_equal(full[1000:2500], part)
     T = lp.dense_tableau("degenerate", 2, 50, 30)
     assert T.shape == (51, 31) and np.all(T[-1, 30] == 0)
+
+
+def _integration_stub():
+    """The ctypes binding block of INTEGRATION.md, bound to the in-tree libsmx.so."""
+    from simplex_mi355x import _lib
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = re.search(r"```python\n(# src/simplex_hip.py.*?)```", text, flags=re.S).group(1)
+    ns = {}
+    exec(compile(block.replace('"libsmx.so"', repr(_lib.LIB_PATH)), "INTEGRATION.md", "exec"),
+         ns)
+    return ns
+
+
+def test_integration_stub_matches_library_signatures():
+    from simplex_mi355x import _lib
+    ns = _integration_stub()
+    L = _lib.load()
+    for name in ("smx_reset", "smx_select", "smx_finalize", "smx_update", "smx_run"):
+        stub = getattr(ns["L"], name).argtypes
+        assert len(stub) == len(getattr(L, name).argtypes), name
+    assert ctypes.sizeof(ns["Shape"]) == ctypes.sizeof(_lib.Shape)

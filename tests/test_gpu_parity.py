@@ -361,3 +361,23 @@ def test_fused_chain_matches_unfused_on_every_fixture():
     finally:
         L.smx_tune_fused(1)
     assert n_checked > 250
+
+
+# ----------------------------------------------------------------------------------------------
+# 11. the maintainer-side ctypes stub printed in INTEGRATION.md runs the engine correctly
+def test_integration_stub_pivot_loop_vs_oracle():
+    import torch
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    from test_abi import _integration_stub
+    ns = _integration_stub()
+    n, m, k = 300, 200, 60
+    T = lp.dense_tableau("uniform", 3, n, m)
+    buf, c, log = ns["pivot_loop"](T[:n].tolist(), T[n, :m].tolist(), k)
+    torch.cuda.synchronize()
+    Tref, st, done, lref = c_oracle.run(T, n, m, m, k)
+    npiv = int(c[5])
+    assert npiv == done
+    assert np.array_equal(log.cpu().numpy().reshape(-1, 2)[:done], lref)
+    got = buf[npiv & 1].cpu().numpy()
+    assert np.array_equal(got[:n, :m + 1].view(np.int64), Tref[:n, :m + 1].view(np.int64))

@@ -1,7 +1,9 @@
 """GPU: the HIP shard kernels for P simulated ranks in one process on one device (the all-gather
-done by a device copy), against the unsharded C oracle, bit for bit -- both pivot forms: unfused
-(k_select/k_pack/k_update<kShard>) and fused (k_la_prime/k_pack<fused>/k_update<kShardFused>).  The multi-process RCCL path itself is covered by bench.py --sharded (world 1 on the
-test box) and by the gloo tests of the same driver."""
+done by a device copy), against the unsharded C oracle, bit for bit -- all three pivot forms:
+unfused (k_select/k_pack/k_update<kShard>), fused (k_la_prime/k_pack<fused>/
+k_update<kShardFused>) and the overlapped chain's halves (k_shard_la + k_pack_ahead, then the
+sweep without look-ahead workgroups).  The native RCCL driver is covered at world size 1
+(tools/check_native_shard.py) and the multi-process protocol by the gloo tests."""
 from __future__ import annotations
 
 import numpy as np
@@ -17,7 +19,10 @@ def _need_gpu():
         pytest.skip("needs an MI355X")
 
 
-def _simulate(T, n, m, k, P, fused=True, bes=None):
+MODES = {"overlap": (True, True), "fused": (True, False), "unfused": (False, False)}
+
+
+def _simulate(T, n, m, k, P, mode="overlap", bes=None):
     import torch
     from simplex_mi355x.sharded import HipShardBackend, row_range
     if bes is None:
@@ -25,7 +30,8 @@ def _simulate(T, n, m, k, P, fused=True, bes=None):
         for p in range(P):
             lo, hi = row_range(n, p, P)
             local = np.concatenate([T[lo:hi], T[n:n + 1]], axis=0)
-            bes.append(HipShardBackend(local, n, m, m, lo, P, fused=fused))
+            fused, overlap = MODES[mode]
+            bes.append(HipShardBackend(local, n, m, m, lo, P, fused=fused, overlap=overlap))
     for _ in range(k):
         for be in bes:
             with be.stream_ctx():
@@ -46,7 +52,7 @@ def _simulate(T, n, m, k, P, fused=True, bes=None):
     return states, logs, tables, full, bes
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("kind,n,m,k,P", [
     ("uniform", 1023, 1023, 80, 2),
     ("uniform", 1001, 777, 80, 3),
@@ -57,11 +63,11 @@ def _simulate(T, n, m, k, P, fused=True, bes=None):
     ("uniform", 40, 30, 78, 3),   # step 26 pivots on row 26 = rank 2's first row: on rank 1
                                   # r - row0 == its f-row replica's local index (regression)
 ])
-def test_hip_shards_match_oracle(kind, n, m, k, P, fused):
+def test_hip_shards_match_oracle(kind, n, m, k, P, mode):
     from oracle import c_oracle
     from simplex_mi355x import lp
     T = lp.dense_tableau(kind, 7, n, m)
-    states, logs, tables, full, _ = _simulate(T, n, m, k, P, fused)
+    states, logs, tables, full, _ = _simulate(T, n, m, k, P, mode)
     Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
     for s, lg in zip(states, logs):
         assert s["npivots"] == done
@@ -72,14 +78,14 @@ def test_hip_shards_match_oracle(kind, n, m, k, P, fused):
     assert np.array_equal(full[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_hip_shards_terminal_outcome(fused):
+@pytest.mark.parametrize("mode", list(MODES))
+def test_hip_shards_terminal_outcome(mode):
     """A run that ends (optimum or error) stops identically on every rank."""
     from oracle import c_oracle
     from simplex_mi355x import lp
     n, m = 40, 30
     T = lp.dense_tableau("uniform", 2, n, m)
-    states, logs, tables, full, _ = _simulate(T, n, m, 400, 3, fused)
+    states, logs, tables, full, _ = _simulate(T, n, m, 400, 3, mode)
     Tref, st, done, log = c_oracle.run(T, n, m, m, 400)
     assert done < 400
     for s in states:
@@ -106,13 +112,13 @@ def test_hip_shards_fused_then_unfused():
     from simplex_mi355x import _lib, lp
     n, m, P = 600, 500, 3
     T = lp.dense_tableau("mixed", 11, n, m)
-    _, _, _, _, bes = _simulate(T, n, m, 37, P, fused=True)
+    _, _, _, _, bes = _simulate(T, n, m, 37, P, mode="fused")
     L = _lib.load()
     for be in bes:
         d = be.dev
         _lib.check(L.smx_fused_publish(ctypes.byref(be._shape), d.step & 1, d.ctl.data_ptr(),
                                        d.parts.data_ptr(), d.stream.cuda_stream), "publish")
-        be.fused = False
+        be.fused = be.overlap = False
     torch.cuda.synchronize()
     states, logs, tables, full, _ = _simulate(T, n, m, 45, P, bes=bes)
     Tref, st, done, log = c_oracle.run(T, n, m, m, 82, threads=8)

@@ -21,9 +21,10 @@ dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
 ok = True
 cases = (("uniform", 1023, 777, 120), ("mixed", 600, 500, 150),
          ("degenerate", 300, 300, 100), ("uniform", 40, 30, 400))
-for fused, (kind, n, m, k) in [(f, c) for f in (True, False) for c in cases]:
+modes = (("overlap", True, True), ("fused", True, False), ("unfused", False, False))
+for (mode, fused, overlap), (kind, n, m, k) in [(md, c) for md in modes for c in cases]:
     T = lp.dense_tableau(kind, 5, n, m)
-    be = HipShardBackend(T, n, m, m, 0, 1, device="cuda:0", fused=fused)
+    be = HipShardBackend(T, n, m, m, 0, 1, device="cuda:0", fused=fused, overlap=overlap)
     comm = RcclComm()
     st = ShardedSolver(be, comm=comm).run(k)
     Tref, s_ref, done, log = c_oracle.run(T, n, m, m, k, threads=8)
@@ -31,7 +32,7 @@ for fused, (kind, n, m, k) in [(f, c) for f in (True, False) for c in cases]:
     same = (st["npivots"] == done and np.array_equal(be.log(0, done), log)
             and np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
             and (not st["term"] or st["status"] == s_ref))
-    print("fused" if fused else "unfused", kind, n, m, "pivots", st["npivots"], done,
+    print(mode, kind, n, m, "pivots", st["npivots"], done,
           "ok" if same else "MISMATCH", flush=True)
     ok &= same
     comm.close()
