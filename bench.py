@@ -88,25 +88,100 @@ def cycle_report(n, m, log):
     return None if tr.cycle is None else {"first_step": tr.cycle[0], "period": tr.cycle[1]}
 
 
-def cpu_baseline(T, n, m, seconds):
-    """numpy port (oracle/numpy_oracle.py) timed on this host, 1 thread, bounded sample."""
-    import numpy as np
-    from oracle import numpy_oracle
-    A = np.ascontiguousarray(T)
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _timed_pivots(pick, pivot, A, n, m, seconds, min_done=2):
     done = 0
     t0 = time.perf_counter()
     while True:
-        st, r, c = numpy_oracle.pick(A, n, m, m)
-        if st != numpy_oracle.PIVOT:
+        st, r, c = pick(A, n, m, m)
+        if st != 0:
             break
-        A = numpy_oracle.pivot(A, r, c)
+        A = pivot(A, r, c)
         done += 1
-        if time.perf_counter() - t0 >= seconds and done >= 2:
+        if time.perf_counter() - t0 >= seconds and done >= min_done:
             break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "pivots/s", "cores": 1, "kind": "port",
-            "sample": f"{done} pivots of the same {n + 1}x{m + 1} tableau from step 0 "
-                      f"(numpy restatement, single thread), {dt:.1f} s"}
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(T, n, m, seconds):
+    """The reference's CPU path, restated (it is pure Python and cannot ship to the GPU box),
+    timed on this host on a bounded sample of the same workload:
+      value  -- numpy port (oracle/numpy_oracle.py, bit-identical), 1 thread, ~`seconds` s;
+      omp    -- C port (oracle/simplex_oracle.c, bit-identical), OpenMP on the CPU share;
+      python -- pure-Python list restatement incl. deepcopy (oracle/restated.py, the reference's
+                own algorithm) at 1024x1024, its ns/element scaled to this tableau."""
+    import numpy as np
+    from oracle import c_oracle, numpy_oracle, restated
+    A = np.ascontiguousarray(T)
+    done, dt = _timed_pivots(numpy_oracle.pick, numpy_oracle.pivot, A, n, m, seconds)
+    out = {"value": done / dt, "unit": "pivots/s", "cores": 1, "kind": "port",
+           "sample": f"{done} pivots of the same {n + 1}x{m + 1} tableau from step 0 "
+                     f"(numpy restatement, single thread), {dt:.1f} s",
+           "cpu_model": _cpu_model()}
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16"))))
+    done_c, dt_c = _timed_pivots(
+        c_oracle.pick, lambda X, r, c: c_oracle.pivot(X, r, c, threads=threads), A, n, m,
+        seconds / 3)
+    out["omp"] = {"value": done_c / dt_c, "unit": "pivots/s", "cores": threads, "kind": "port",
+                  "sample": f"{done_c} pivots, C restatement with OpenMP, {dt_c:.1f} s"}
+    # pure Python on a 1024^2 replica of the generator (the reference's own per-element cost)
+    from simplex_mi355x import lp
+    nn = mm = 1023
+    S = lp.dense_tableau("uniform", 0, nn, mm)
+    tab = [list(map(float, row)) for row in S[:nn]] + [list(map(float, S[nn, :mm]))]
+    t0 = time.perf_counter()
+    k = 0
+    while k < 2:
+        st = restated.pick(tab, nn, mm, 1 + max(nn, mm))
+        if st[0] != "pivot":
+            break
+        tab = restated.pivot(tab, st[1], st[2])
+        k += 1
+    dt_p = time.perf_counter() - t0
+    if k:
+        ns_el = dt_p / k / ((nn + 1) * (mm + 1)) * 1e9
+        out["python"] = {"value": 1e9 / (ns_el * (n + 1) * (m + 1)), "unit": "pivots/s",
+                         "cores": 1, "kind": "port",
+                         "sample": f"{k} pivots (pick + pivot with deepcopy) at 1024x1024: "
+                                   f"{ns_el:.0f} ns/element, scaled to {n + 1}x{m + 1}"}
+    return out
+
+
+def copy_ceiling(nbytes):
+    """Best read+write rate of smx_copy_probe on this GPU for nbytes per buffer (GB/s)."""
+    import torch
+    from simplex_mi355x import _lib
+    L = _lib.load()
+    nd = (int(nbytes) // 16) * 2
+    a = torch.ones(nd, dtype=torch.float64, device="cuda")
+    b = torch.empty_like(a)
+    s = torch.cuda.current_stream()
+    best = 0.0
+    for variant in (0, 1):
+        for _ in range(3):
+            _lib.check(L.smx_copy_probe(a.data_ptr(), b.data_ptr(), nd, variant, s.cuda_stream),
+                       "smx_copy_probe")
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(10):
+            L.smx_copy_probe(a.data_ptr(), b.data_ptr(), nd, variant, s.cuda_stream)
+        e1.record(s)
+        torch.cuda.synchronize()
+        best = max(best, 2.0 * nd * 8 / (e0.elapsed_time(e1) / 10) / 1e6)
+    del a, b
+    torch.cuda.empty_cache()
+    return best
 
 
 def run_single(args):
@@ -144,6 +219,7 @@ def run_single(args):
     achieved = bytes_per_pivot / avg_upd / 1e9
     workload = f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
     traffic = load_traffic(args.traffic, f"{R}x{C}")
+    copy_gbs = copy_ceiling(16.0 * R * C / 2)   # same bytes as one pivot (outside timing)
     out = {
         "metric": METRIC,
         "value": args.steps / wall,
@@ -166,7 +242,8 @@ def run_single(args):
                      "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "kernel": "k_update<kFused>" if fused else "k_update<kSingle>",
                      "algorithmic_bytes_per_launch": bytes_per_pivot,
-                     "avg_kernel_ms": avg_upd * 1e3},
+                     "avg_kernel_ms": avg_upd * 1e3,
+                     "copy_ceiling_gbs": copy_gbs, "frac_of_copy": achieved / copy_gbs},
         "trajectory_valid": bool(valid),
         "basis_cycle": cycle,
     }

@@ -219,6 +219,12 @@ int smx_shard_fused_finish(const double* Tin, double* Tout, const double* recv, 
                            void* stream);
 int smx_fused_publish(const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                       const smx_part* parts, void* stream);
+/* Streaming copy of `ndoubles` (even) doubles src -> dst, for measuring the box's read+write
+ * ceiling beside the update (bench.py): variant 0 = 4 x 16-B loads in flight per lane, 256
+ * threads x 1 block per CU; variant 1 = 1 load, 1024 threads x 1 block per CU. */
+int smx_copy_probe(const double* src, double* dst, int64_t ndoubles, int32_t variant,
+                   void* stream);
+
 /* The two halves of a step of the overlapped chain (smx_shard_run's default form), for callers
  * that drive the exchange themselves: after step k's all-gather into `recv`,
  * smx_shard_ahead computes step k+1's records (parts slot parity^1) and packs step k+1's header

@@ -1137,6 +1137,23 @@ __global__ __launch_bounds__(kUpdBlock) void k_pack_ahead(
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_copy: the box's streaming read+write ceiling, measured next to the update in bench.py
+// (the best shapes of tools/hbm_probe.hip: a grid-stride copy with U 16-B loads per lane).
+template <int U>
+__global__ void k_copy(const dbl2* __restrict__ a, dbl2* __restrict__ b, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t st = (int64_t)gridDim.x * blockDim.x;
+    for (; i + (U - 1) * st < n; i += U * st) {
+        dbl2 v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = a[i + k * st];
+#pragma unroll
+        for (int k = 0; k < U; ++k) b[i + k * st] = v[k];
+    }
+    for (; i < n; i += st) b[i] = a[i];
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_batch: many small LPs, one wavefront each (the UI's workload, m = 2,
 // n = 3..20, main.py:309-313).  Lane i holds row i of its LP in registers (rows 0..n, the
 // f-row is lane n), so the whole get_solution loop (simplex.py:184-198) runs inside one launch:
@@ -2027,6 +2044,20 @@ int smx_shard_sweep(const double* Tin, double* Tout, const double* recv, int32_t
     if (!shape_ok(shape) || Tin == Tout || nranks < 1) return (int)hipErrorInvalidValue;
     return launch_sweep(Tin, Tout, *shape, parity & 1, recv, nranks, ctl, log, log_cap, 0,
                         S(stream));
+}
+
+int smx_copy_probe(const double* src, double* dst, int64_t ndoubles, int32_t variant,
+                   void* stream) {
+    if (!src || !dst || ndoubles < 2 || (ndoubles & 1) || variant < 0 || variant > 1)
+        return (int)hipErrorInvalidValue;
+    const int64_t n2 = ndoubles / 2;
+    const auto* a = reinterpret_cast<const dbl2*>(src);
+    auto* b = reinterpret_cast<dbl2*>(dst);
+    if (variant == 0)
+        hipLaunchKernelGGL(k_copy<4>, dim3(num_cus()), dim3(256), 0, S(stream), a, b, n2);
+    else
+        hipLaunchKernelGGL(k_copy<1>, dim3(num_cus()), dim3(1024), 0, S(stream), a, b, n2);
+    return (int)hipGetLastError();
 }
 
 int smx_fused_publish(const smx_shape* shape, int32_t parity, smx_ctl* ctl,

@@ -49,6 +49,7 @@ EXPORTS = (
     "smx_shard_run", "smx_shard_run_timed", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
     "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
     "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
+    "smx_copy_probe",
 )
 
 
@@ -108,6 +109,7 @@ def load():
         "smx_fused_publish": ([sp, i32, vp, vp, vp], ctypes.c_int),
         "smx_shard_ahead": ([vp, sp, i32, vp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_sweep": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
+        "smx_copy_probe": ([vp, vp, i64, i32, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -40,11 +40,13 @@ def objective(kind: str, seed: int, m: int) -> np.ndarray:
 
 
 def dense_rows(kind: str, seed: int, n: int, m: int, row_lo: int = 0, row_hi: int | None = None,
-               ld: int | None = None) -> np.ndarray:
-    """Constraint rows [row_lo, row_hi) of the global n x (m+1) LP, width ld (zero padded)."""
+               ld: int | None = None, out: np.ndarray | None = None) -> np.ndarray:
+    """Constraint rows [row_lo, row_hi) of the global n x (m+1) LP, width ld (zero padded);
+    written into ``out`` (shape (row_hi - row_lo, >= m+1), zero padded by the caller) if given."""
     row_hi = n if row_hi is None else row_hi
     width = m + 1 if ld is None else ld
-    out = np.zeros((row_hi - row_lo, width), dtype=np.float64)
+    if out is None:
+        out = np.zeros((row_hi - row_lo, width), dtype=np.float64)
     k0, k1 = row_lo // BLOCK, (row_hi + BLOCK - 1) // BLOCK
     for k in range(k0, k1):
         lo, hi = k * BLOCK, min(n, (k + 1) * BLOCK)
@@ -57,9 +59,10 @@ def dense_rows(kind: str, seed: int, n: int, m: int, row_lo: int = 0, row_hi: in
 
 def dense_tableau(kind: str, seed: int, n: int, m: int, row_lo: int = 0,
                   row_hi: int | None = None) -> np.ndarray:
-    """Rows [row_lo, row_hi) plus the f-row (objective, len m) as the last row."""
-    rows = dense_rows(kind, seed, n, m, row_lo, row_hi)
-    T = np.zeros((rows.shape[0] + 1, m + 1), dtype=np.float64)
-    T[:-1] = rows
+    """Rows [row_lo, row_hi) plus the f-row (objective, len m) as the last row (one allocation:
+    a 65536 x 32768 tableau is 17 GB)."""
+    row_hi = n if row_hi is None else row_hi
+    T = np.zeros((row_hi - row_lo + 1, m + 1), dtype=np.float64)
+    dense_rows(kind, seed, n, m, row_lo, row_hi, out=T[:-1])
     T[-1, :m] = objective(kind, seed, m)
     return T
