@@ -541,31 +541,19 @@ __device__ void la_partial(const double* __restrict__ T, int64_t ld, int rows, i
 // Fused-chain decision of step k (simplex.py:70-141) from its look-ahead records and T_k: the
 // phase-1 row is the minimum of the records' p1col; its first positive entry is scanned by the
 // whole block on the materialised T_k (:81-85); phase 2 reduces the ratio partials (:105-141).
+// `rec` / `c`: lane k's record (k < nparts <= 64) and the entering column, loaded by wave 0
+// before the sweep's prefetch so the decision does not wait behind it.
 template <int NT>
-__device__ Decision decide_fused(const smx_ctl* __restrict__ ctl,
-                                 const smx_part* __restrict__ parts, int nparts, int parity,
-                                 int n, int m, int flen, const double* __restrict__ T, int64_t ld,
-                                 int* negb_out) {
+__device__ Decision decide_fused(const smx_part& rec, int c, int n, int m, int flen,
+                                 const double* __restrict__ T, int64_t ld, int* negb_out) {
     __shared__ int s_tmp[NT / kWave];
     __shared__ Decision s_d;
     __shared__ int s_negb;
     const int tid = threadIdx.x;
     if (tid < kWave) {
-        // one pass over the records (nparts <= 64: one per lane) and the entering column
-        const int c = ctl->negf[parity];
-        int nb = SMX_NONE;
-        First f{SMX_NONE, 0.0};
-        Cand b = cand_none();
-        for (int k = tid; k < nparts; k += kWave) {
-            const smx_part p = parts[k];
-            nb = min(nb, p.p1col);
-            if (p.first < f.idx) {
-                f.idx = p.first;
-                f.v = p.first_v;
-            }
-            Cand o{p.best_cls, p.best_i, p.best_v};
-            if (better(o, b)) b = o;
-        }
+        int nb = rec.p1col;
+        First f{rec.first, rec.first_v};
+        Cand b{rec.best_cls, rec.best_i, rec.best_v};
         nb = wave_min_int(nb);
         Decision d;
         d.c = c;
@@ -660,6 +648,23 @@ __global__ __launch_bounds__(kWave) void k_publish(const smx_part* __restrict__ 
 // forced_c).
 enum UpdMode { kSingle = 0, kShard = 1, kForced = 2, kFused = 3, kShardFused = 4 };
 
+#ifdef SMX_TRACE
+// Diagnostic build only (tools/trace_fused.hip): per-workgroup s_memrealtime stamps (100 MHz,
+// chip-wide) of the last two update launches, [launch parity][block][phase]:
+// 0 entry, 1 decision known, 2 look-ahead records written, 3 sweep done.
+constexpr int kTraceBlocks = 4096;
+__device__ unsigned long long g_trace[2][kTraceBlocks][4];
+#define SMX_STAMP(ph)                                                                  \
+    do {                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks)                             \
+            g_trace[parity & 1][blockIdx.x][ph] = __builtin_amdgcn_s_memrealtime();    \
+    } while (0)
+#else
+#define SMX_STAMP(ph) \
+    do {              \
+    } while (0)
+#endif
+
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 template <bool NTL>
@@ -688,6 +693,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     if (MODE != kForced && ctl->term) return;
+    SMX_STAMP(0);
     const int R = rows_local + 1;  // + the f-row (local row rows_local)
     const int C = m + 1;
     constexpr int kChunk = kWave * 2;                  // doubles per unit
@@ -730,6 +736,12 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
             if (b.i[k] < R && j < C) b.x[k] = ld2<NTL>(Tin + (int64_t)b.i[k] * ld + j);
         }
     };
+    smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
+    int negf0 = SMX_NONE;
+    if (MODE == kFused && tid < kWave) {   // the decision's loads first (in-order vmcnt)
+        if (tid < nparts) rec = parts[(size_t)parity * nparts + tid];
+        negf0 = ctl->negf[parity];
+    }
     Batch<U> cur;
     if (sweeps) fetch(cur);
 
@@ -743,8 +755,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         Decision dd;
         int negb_f = SMX_NONE;
         if (MODE == kFused)   // whole block (phase-1 row scan); parts = this step's slot
-            dd = decide_fused<kUpdBlock>(ctl, parts + (size_t)parity * nparts, nparts, parity,
-                                         n, m, flen, Tin, ld, &negb_f);
+            dd = decide_fused<kUpdBlock>(rec, negf0, n, m, flen, Tin, ld, &negb_f);
         if (tid < kWave) {
             Decision d;
             if (MODE == kFused)
@@ -805,6 +816,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         prow = recv + s_off;
     }
     const double e = prow[c];
+    SMX_STAMP(1);
     // history: rows whose new "-b" entry is x1 / x2 of the new tableau (find_optimum)
     int hx0 = -1, hx1 = -1;
     int64_t hslot = 0;
@@ -821,6 +833,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         la_partial<kUpdBlock, true>(Tin, ld, rows_local, m, fscan, row0, r_local, c, e, prow,
                                     const_cast<smx_part*>(parts) + (size_t)(parity ^ 1) * nparts,
                                     blockIdx.x, nparts, ctl, parity ^ 1);
+        SMX_STAMP(2);
         if (!la_sweep) return;
     }
     int ch_pr = -1;
@@ -889,6 +902,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
             fetch(cur);
         }
     }
+    SMX_STAMP(3);
     if (MODE == kSingle || MODE == kShard) {
         lb = wave_min_int(lb);
         lf = wave_min_int(lf);
