@@ -130,6 +130,16 @@ def fused_enabled() -> bool:
     return bool(load().smx_tune_fused(-1))
 
 
+NCCL_RESULTS = {1: "ncclUnhandledCudaError", 2: "ncclSystemError", 3: "ncclInternalError",
+                4: "ncclInvalidArgument", 5: "ncclInvalidUsage (e.g. two ranks on one GPU)",
+                6: "ncclRemoteError", 7: "ncclInProgress"}
+
+
 def check(err: int, what: str) -> None:
-    if err != 0:
-        raise RuntimeError(f"{what} failed with hipError {err}")
+    """Raise on a libsmx error: hipError_t codes, or -1000 - ncclResult_t for RCCL failures."""
+    if err == 0:
+        return
+    if err <= -1000:
+        code = -1000 - err
+        raise RuntimeError(f"{what} failed: RCCL {NCCL_RESULTS.get(code, code)}")
+    raise RuntimeError(f"{what} failed with hipError {err}")

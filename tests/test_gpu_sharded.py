@@ -62,6 +62,8 @@ def _simulate(T, n, m, k, P, mode="overlap", bes=None):
     ("degenerate_mixed", 300, 500, 120, 5),
     ("uniform", 40, 30, 78, 3),   # step 26 pivots on row 26 = rank 2's first row: on rank 1
                                   # r - row0 == its f-row replica's local index (regression)
+    ("mixed", 5, 7, 30, 8),       # fewer constraint rows than ranks: some ranks own none
+    ("degenerate_mixed", 9, 3, 40, 4),
 ])
 def test_hip_shards_match_oracle(kind, n, m, k, P, mode):
     from oracle import c_oracle
@@ -126,3 +128,36 @@ def test_hip_shards_fused_then_unfused():
         assert s_["npivots"] == done
         assert np.array_equal(lg, log)
     assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))
+
+
+def _nan_tables():
+    """The gloo tests' NaN cases (simplex.py:117-121: a NaN first candidate sticks; a NaN that
+    is not the global first candidate is ignored)."""
+    n, m = 6, 3
+    A = np.zeros((n + 1, m + 1))
+    A[:, :m] = [[0, 1, 1], [0, -1, 2], [0, 1, -1], [np.nan, 1, 1], [-1, 1, 1], [-2, 1, 1],
+                [-1, -1, -1]]
+    A[:n, m] = [1, 2, 3, 1, 1, 1]
+    n2, m2 = 6, 2
+    B = np.zeros((n2 + 1, m2 + 1))
+    B[:n2, 0] = [0, 0, -4, np.nan, -1, -3]
+    B[:n2, 1] = [1, 1, 1, 1, 1, 1]
+    B[:n2, m2] = [1, 1, 8, 1, 1, 1]
+    B[n2, :m2] = [-1, -1]
+    return [(A, n, m), (B, n2, m2)]
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("case", [0, 1])
+@pytest.mark.parametrize("P", [2, 3])
+def test_hip_shards_nan_first_candidate(mode, case, P):
+    from oracle import c_oracle
+    T, n, m = _nan_tables()[case]
+    states, logs, tables, full, _ = _simulate(T, n, m, 3, P, mode)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, 3)
+    for s_, lg in zip(states, logs):
+        assert s_["npivots"] == done
+        assert np.array_equal(lg, log)
+    assert np.array_equal(np.nan_to_num(full[:n]).view(np.int64),
+                          np.nan_to_num(Tref[:n]).view(np.int64))
+    assert np.array_equal(np.isnan(full[:n]), np.isnan(Tref[:n]))

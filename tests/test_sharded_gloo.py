@@ -65,6 +65,7 @@ CASES = [
     ("mixed", 47, 33, 80, 3),
     ("degenerate", 40, 30, 60, 2),
     ("degenerate_mixed", 45, 25, 60, 3),
+    ("mixed", 2, 6, 20, 3),           # fewer constraint rows than ranks: rank 0 owns none
 ]
 
 
