@@ -62,7 +62,7 @@ typedef struct smx_ctl {
     double sel_e;       /* last selection: pivot element T[r][c]                              */
     int64_t npivots;    /* pivots applied since smx_reset(..., clear_count=1)                 */
     int32_t sel_owner;  /* sharded: rank whose candidate row is the pivot row                 */
-    int32_t pad0;
+    int32_t nla;        /* sharded fused update: look-ahead workgroups done (0 between launches) */
     int64_t shard_off;  /* sharded: offset (doubles) of the pivot row in the receive buffer   */
     int32_t xpos[2][2]; /* [parity][x1, x2]: position code of labels 'x1', 'x2' (simplex.py:
                            58-59): p >= 0 row p (basic), -(j+1) column j, SMX_ABSENT none      */
@@ -207,16 +207,19 @@ int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_
 /* The same pivot with the fused look-ahead (no select kernel): smx_shard_fused_begin packs the
  * header and candidate rows from this step's look-ahead records (parts slot `parity`, written by
  * smx_shard_fused_prime for the first step of a sequence, by the previous fused finish after
- * that); smx_shard_fused_finish merges, updates and writes the next step's records.  Before
- * switching back to the unfused calls, smx_fused_publish(next parity) restores ctl->negb. */
+ * that); smx_shard_fused_finish merges, updates and writes the next step's records -- and, when
+ * `send` is not NULL and smx_shard_folds_pack(shape) (local buffer >= 64 MiB, where the sweep
+ * hides it), already packs the next step into it: then skip the next begin.  Before switching
+ * back to the unfused calls, smx_fused_publish(next parity) restores ctl->negb. */
+int smx_shard_folds_pack(const smx_shape* shape);
 int smx_shard_fused_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                           smx_part* parts, void* stream);
 int smx_shard_fused_begin(const double* T, const smx_shape* shape, int32_t parity,
                           const smx_ctl* ctl, const smx_part* parts, double* send, void* stream);
 int smx_shard_fused_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
                            const smx_shape* shape, int32_t parity, smx_ctl* ctl, smx_part* parts,
-                           int32_t* log, int64_t log_cap, void* ev_before, void* ev_after,
-                           void* stream);
+                           double* send, int32_t* log, int64_t log_cap, void* ev_before,
+                           void* ev_after, void* stream);
 int smx_fused_publish(const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                       const smx_part* parts, void* stream);
 /* Streaming copy of `ndoubles` (even) doubles src -> dst, for measuring the box's read+write
@@ -240,7 +243,8 @@ int smx_shard_sweep(const double* Tin, double* Tout, const double* recv, int32_t
 /* Native RCCL driver (one communicator per rank; the unique id is created on rank 0 and
  * shipped to the others by any bootstrap, e.g. torch.distributed.broadcast_object_list).
  * smx_shard_run = k x {select, pack, ncclAllGather on `stream`, update}; with smx_tune_fused(1)
- * (the default) prime + k x {fused pack, ncclAllGather, fused update} + publish; with
+ * (the default) prime + pack + k x {ncclAllGather, fused update that also packs the next step}
+ * + publish; with
  * smx_tune_fused(2) the overlapped form: the update sweeps on `stream` while an internal exchange
  * stream computes the next step's look-ahead records, header and candidate rows from T_k and
  * gathers them (two events per step).  No host synchronisation.  `recv` must hold

@@ -298,6 +298,7 @@ __global__ __launch_bounds__(1024) void k_reset(const double* __restrict__ T, in
         ctl->negb[parity ^ 1] = SMX_NONE;
         ctl->negf[parity ^ 1] = SMX_NONE;
         ctl->term = 0;
+        ctl->nla = 0;
         ctl->sel_status = SMX_IDLE;
         ctl->sel_r = SMX_NONE;
         ctl->sel_c = SMX_NONE;
@@ -626,6 +627,87 @@ __global__ __launch_bounds__(kWave) void k_publish(const smx_part* __restrict__ 
     }
 }
 
+// Header + candidate rows of step k+1 (layout of k_pack) from step k+1's records (`parts`, slot
+// `slot`, nparts of them) and T_k with step k's pivot (r_local, c, e, prow): every value is
+// nv(T_k, pivot k), i.e. exactly T_{k+1}.  Workgroup bidx of nblk; all threads of the group call.
+__device__ void pack_ahead(const double* __restrict__ T, int64_t ld, int rows, int m, int row0,
+                           int r_local, int c, double e, const double* __restrict__ prow,
+                           const smx_ctl* __restrict__ ctl, const smx_part* __restrict__ parts,
+                           int nparts, int slot, double* __restrict__ send, int bidx, int nblk) {
+    __shared__ int s_rows[2];
+    __shared__ int s_hdr_i[4];
+    __shared__ double s_hdr_d[2];
+    __shared__ int s_tmp[kUpdBlock / kWave];
+    const int tid = threadIdx.x;
+    const int cn = ctl->negf[slot];   // step k+1's entering column (look-ahead workgroup 0)
+    if (tid < kWave) {
+        int nb = SMX_NONE;
+        First f{SMX_NONE, 0.0};
+        Cand b = cand_none();
+        for (int k = tid; k < nparts; k += kWave) {
+            const smx_part p = parts[k];
+            nb = min(nb, p.p1col);
+            if (p.first < f.idx) {
+                f.idx = p.first;
+                f.v = p.first_v;
+            }
+            Cand o{p.best_cls, p.best_i, p.best_v};
+            if (better(o, b)) b = o;
+        }
+        nb = wave_min_int(nb);
+        f = wave_first(f);
+        b = wave_best(b);
+        if (nb != SMX_NONE || cn == SMX_NONE) {   // phase 1 / no entering column: no ratio test
+            f = First{SMX_NONE, 0.0};
+            b = cand_none();
+        }
+        if (tid == 0) {
+            s_rows[0] = (f.idx != SMX_NONE && isnan(f.v)) ? f.idx - row0 : -1;     // row A
+            s_rows[1] = (nb != SMX_NONE) ? nb - row0 : (b.cls < 3 ? b.idx - row0 : -1);
+            s_hdr_i[0] = nb;
+            s_hdr_i[1] = f.idx;
+            s_hdr_i[2] = b.cls;
+            s_hdr_i[3] = b.idx;
+            s_hdr_d[0] = f.v;
+            s_hdr_d[1] = b.v;
+        }
+    }
+    __syncthreads();
+    const int ra = s_rows[0], rb = s_rows[1];
+    const int nb = s_hdr_i[0];
+    if (bidx == 0) {
+        int p1 = SMX_NONE;   // phase 1 (simplex.py:81-85) on the new values of the owner's row
+        if (nb != SMX_NONE) {
+            const int il = nb - row0;
+            const double pci = T[(int64_t)il * ld + c];
+            for (int j = tid; j < m; j += kUpdBlock) {
+                if (nv(T, ld, r_local, c, e, prow, il, j, pci) > 0.0) {
+                    p1 = j;
+                    break;
+                }
+            }
+            p1 = block_min_int<kUpdBlock>(p1, s_tmp);
+        }
+        if (tid == 0) {
+            send[0] = (double)nb;
+            send[1] = (double)s_hdr_i[1];
+            send[2] = s_hdr_d[0];
+            send[3] = (double)s_hdr_i[2];
+            send[4] = (double)s_hdr_i[3];
+            send[5] = s_hdr_d[1];
+            send[6] = (double)cn;
+            send[7] = (double)p1;
+        }
+    }
+    const int C = m + 1;
+    const double pca = ra >= 0 ? T[(int64_t)ra * ld + c] : 0.0;
+    const double pcb = rb >= 0 ? T[(int64_t)rb * ld + c] : 0.0;
+    for (int j = bidx * kUpdBlock + tid; j < C; j += nblk * kUpdBlock) {
+        if (ra >= 0) send[SMX_SHARD_HDR + j] = nv(T, ld, r_local, c, e, prow, ra, j, pca);
+        if (rb >= 0) send[SMX_SHARD_HDR + ld + j] = nv(T, ld, r_local, c, e, prow, rb, j, pcb);
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_update: the modified Jordan step (simplex.py:149-177), out of place.
 //
@@ -688,7 +770,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
     int n, int m, int flen, int fscan, int row0, int parity, smx_ctl* __restrict__ ctl,
     const smx_part* __restrict__ parts, int nparts, int32_t* __restrict__ log,
     double* __restrict__ xhist, int64_t log_cap, const double* __restrict__ recv, int forced_r,
-    int forced_c) {
+    int forced_c, double* __restrict__ send) {
     __shared__ int s_dec[3];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -833,6 +915,24 @@ __global__ __launch_bounds__(kUpdBlock) void k_update(
         la_partial<kUpdBlock, true>(Tin, ld, rows_local, m, fscan, row0, r_local, c, e, prow,
                                     const_cast<smx_part*>(parts) + (size_t)(parity ^ 1) * nparts,
                                     blockIdx.x, nparts, ctl, parity ^ 1);
+        if (MODE == kShardFused && send != nullptr) {
+            // The last look-ahead workgroup to finish packs step k+1's header and candidate
+            // rows into the send slot (values of T_{k+1} via nv), so a sharded pivot is this
+            // kernel + the all-gather.  nparts counter atomics, not one per workgroup.
+            __shared__ int s_last;
+            __syncthreads();
+            if (tid == 0) {
+                __threadfence();   // release this workgroup's record (and negf from group 0)
+                s_last = atomicAdd(&ctl->nla, 1) == nparts - 1;
+            }
+            __syncthreads();
+            if (s_last) {
+                __threadfence();   // acquire the other workgroups' records
+                pack_ahead(Tin, ld, rows_local, m, row0, r_local, c, e, prow, ctl,
+                           parts + (size_t)(parity ^ 1) * nparts, nparts, parity ^ 1, send, 0, 1);
+                if (tid == 0) ctl->nla = 0;
+            }
+        }
         SMX_STAMP(2);
         if (!la_sweep) return;
     }
@@ -1062,92 +1162,19 @@ __global__ __launch_bounds__(kUpdBlock) void k_shard_la(const double* __restrict
                                 blockIdx.x, gridDim.x, ctl, slot);
 }
 
-// Header + candidate rows of step k+1 (layout of k_pack) from step k+1's records (`parts`, slot
-// `slot`) and T_k: every value is nv(T_k, pivot k), i.e. exactly T_{k+1}.
 __global__ __launch_bounds__(kUpdBlock) void k_pack_ahead(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int row0,
     const double* __restrict__ recv, int nranks, const smx_ctl* __restrict__ ctl,
     const smx_part* __restrict__ parts, int nparts, int slot, double* __restrict__ send) {
     __shared__ int s_dec[3];
     __shared__ int64_t s_off;
-    __shared__ int s_rows[2];
-    __shared__ int s_hdr_i[4];
-    __shared__ double s_hdr_d[2];
-    __shared__ int s_tmp[kUpdBlock / kWave];
-    const int tid = threadIdx.x;
     if (ctl->term) return;
     if (!merged_pivot(recv, nranks, ld, m, flen, s_dec, &s_off)) return;
     const int r = s_dec[1], c = s_dec[2];
     const double* prow = recv + s_off;
-    const double e = prow[c];
     const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
-    const int cn = ctl->negf[slot];   // step k+1's entering column (k_shard_la, block 0)
-    if (tid < kWave) {
-        int nb = SMX_NONE;
-        First f{SMX_NONE, 0.0};
-        Cand b = cand_none();
-        for (int k = tid; k < nparts; k += kWave) {
-            const smx_part p = parts[k];
-            nb = min(nb, p.p1col);
-            if (p.first < f.idx) {
-                f.idx = p.first;
-                f.v = p.first_v;
-            }
-            Cand o{p.best_cls, p.best_i, p.best_v};
-            if (better(o, b)) b = o;
-        }
-        nb = wave_min_int(nb);
-        f = wave_first(f);
-        b = wave_best(b);
-        if (nb != SMX_NONE || cn == SMX_NONE) {   // phase 1 / no entering column: no ratio test
-            f = First{SMX_NONE, 0.0};
-            b = cand_none();
-        }
-        if (tid == 0) {
-            s_rows[0] = (f.idx != SMX_NONE && isnan(f.v)) ? f.idx - row0 : -1;     // row A
-            s_rows[1] = (nb != SMX_NONE) ? nb - row0 : (b.cls < 3 ? b.idx - row0 : -1);
-            s_hdr_i[0] = nb;
-            s_hdr_i[1] = f.idx;
-            s_hdr_i[2] = b.cls;
-            s_hdr_i[3] = b.idx;
-            s_hdr_d[0] = f.v;
-            s_hdr_d[1] = b.v;
-        }
-    }
-    __syncthreads();
-    const int ra = s_rows[0], rb = s_rows[1];
-    const int nb = s_hdr_i[0];
-    if (blockIdx.x == 0) {
-        int p1 = SMX_NONE;   // phase 1 (simplex.py:81-85) on the new values of the owner's row
-        if (nb != SMX_NONE) {
-            const int il = nb - row0;
-            const double pci = T[(int64_t)il * ld + c];
-            for (int j = tid; j < m; j += kUpdBlock) {
-                if (nv(T, ld, r_local, c, e, prow, il, j, pci) > 0.0) {
-                    p1 = j;
-                    break;
-                }
-            }
-            p1 = block_min_int<kUpdBlock>(p1, s_tmp);
-        }
-        if (tid == 0) {
-            send[0] = (double)nb;
-            send[1] = (double)s_hdr_i[1];
-            send[2] = s_hdr_d[0];
-            send[3] = (double)s_hdr_i[2];
-            send[4] = (double)s_hdr_i[3];
-            send[5] = s_hdr_d[1];
-            send[6] = (double)cn;
-            send[7] = (double)p1;
-        }
-    }
-    const int C = m + 1;
-    const double pca = ra >= 0 ? T[(int64_t)ra * ld + c] : 0.0;
-    const double pcb = rb >= 0 ? T[(int64_t)rb * ld + c] : 0.0;
-    for (int j = blockIdx.x * kUpdBlock + tid; j < C; j += gridDim.x * kUpdBlock) {
-        if (ra >= 0) send[SMX_SHARD_HDR + j] = nv(T, ld, r_local, c, e, prow, ra, j, pca);
-        if (rb >= 0) send[SMX_SHARD_HDR + ld + j] = nv(T, ld, r_local, c, e, prow, rb, j, pcb);
-    }
+    pack_ahead(T, ld, rows, m, row0, r_local, c, prow[c], prow, ctl, parts, nparts, slot, send,
+               blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1379,12 +1406,19 @@ int g_variant = -1;       // smx_tune_set overrides
 constexpr int kLargeVariant = 1, kSmallVariant = 0;
 constexpr int64_t kCacheTable = 16ll << 20;
 constexpr int64_t kLaSweepTable = 256ll << 20;
+// Sharded fused update: its last look-ahead workgroup packs the next step (one workgroup reading
+// two rows) only when the local sweep is long enough to hide that (2048^2 world 1: 27.2 vs
+// 19.0 us per update; 16384^2 world 1: 812 us either way); smaller shards use k_pack<true>.
+constexpr int64_t kFoldPackTable = 64ll << 20;
+inline bool folds_pack(const smx_shape& s) {
+    return (int64_t)(s.rows + 1) * s.ld * 8 >= kFoldPackTable;
+}
 int g_blocks_per_cu = 0;  // 0: kDefaultBpc, capped by the occupancy API (see blocks_per_cu)
 constexpr int kDefaultBpc = 5;
 
 using UpdFn = void (*)(const double*, double*, int64_t, int, int, int, int, int, int, int,
                        smx_ctl*, const smx_part*, int, int32_t*, double*, int64_t, const double*,
-                       int, int);
+                       int, int, double*);
 
 template <int MODE>
 UpdFn upd_fn(int v) {
@@ -1479,7 +1513,7 @@ template <int MODE>
 int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int parity,
                        smx_ctl* ctl, const smx_part* parts, int32_t* log, double* xhist,
                        int64_t log_cap, const double* recv, int fr, int fc, hipStream_t st,
-                       int reserve = 0) {
+                       int reserve = 0, double* send = nullptr) {
     const int v = variant_for(s);
     UpdFn fn = upd_fn<MODE>(v);
     // kFused: the first nparts workgroups compute the look-ahead records; within the Infinity
@@ -1495,7 +1529,7 @@ int launch_update_mode(const double* Tin, double* Tout, const smx_shape& s, int 
     if (LA) fr = la_sweep ? 1 : 0;   // kShardFused: fc = rank count (caller)
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, Tin,
                        Tout, s.ld, s.rows, s.n, s.m, s.flen, fscan_of(s), s.row0, parity, ctl,
-                       parts, s.nparts, log, xhist, log_cap, recv, fr, fc);
+                       parts, s.nparts, log, xhist, log_cap, recv, fr, fc, send);
     return (int)hipGetLastError();
 }
 
@@ -1815,26 +1849,29 @@ int smx_comm_destroy(void* comm) {
 }
 
 namespace {
-// Fused sharded chain, per pivot: k_pack<true> (records of step k -> header + candidate rows of
-// the materialised T_k) -> one ncclAllGather -> k_update<kShardFused> (merge, sweep, records of
-// step k+1).  Primed by k_la_prime, closed by k_publish.  e_upd: 2k events around the updates.
+// Fused sharded chain, per pivot: one ncclAllGather -> k_update<kShardFused> (merge, sweep, the
+// records of step k+1, and -- by its last look-ahead workgroup -- step k+1's header and candidate
+// rows in `send`).  Primed by k_la_prime + k_pack<true>, closed by k_publish.  e_upd: 2k events
+// around the updates.
 int shard_chain_fused(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
                       smx_ctl* ctl, smx_part* parts, double* send, double* recv, int nranks,
                       ncclComm_t comm, int32_t* log, int64_t log_cap, hipEvent_t* e_upd,
                       hipStream_t st) {
-    int err = launch_prime(parity ? buf1 : buf0, s, parity, ctl, parts, st);
+    double* T0 = parity ? buf1 : buf0;
+    const bool fold = folds_pack(s);
+    int err = launch_prime(T0, s, parity, ctl, parts, st);
     const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)s.ld;
     for (int step = 0; step < k && !err; ++step) {
         const int p = (parity + step) & 1;
         double* tin = p ? buf1 : buf0;
         double* tout = p ? buf0 : buf1;
-        err = launch_pack<true>(tin, s, p, ctl, parts + (size_t)p * s.nparts, send, st);
-        if (err) break;
-        err = nccl_err(ncclAllGather(send, recv, slot, ncclFloat64, comm, st));
+        if (step == 0 || !fold)
+            err = launch_pack<true>(tin, s, p, ctl, parts + (size_t)p * s.nparts, send, st);
+        if (!err) err = nccl_err(ncclAllGather(send, recv, slot, ncclFloat64, comm, st));
         if (err) break;
         if (e_upd) (void)hipEventRecord(e_upd[2 * step], st);
         err = launch_update_mode<kShardFused>(tin, tout, s, p, ctl, parts, log, nullptr, log_cap,
-                                              recv, 0, nranks, st);
+                                              recv, 0, nranks, st, 0, fold ? send : nullptr);
         if (e_upd) (void)hipEventRecord(e_upd[2 * step + 1], st);
     }
     if (!err) err = launch_publish(s, (parity + k) & 1, ctl, parts, st);
@@ -2035,15 +2072,20 @@ int smx_shard_fused_begin(const double* T, const smx_shape* shape, int32_t parit
 
 int smx_shard_fused_finish(const double* Tin, double* Tout, const double* recv, int32_t nranks,
                            const smx_shape* shape, int32_t parity, smx_ctl* ctl, smx_part* parts,
-                           int32_t* log, int64_t log_cap, void* ev_before, void* ev_after,
-                           void* stream) {
+                           double* send, int32_t* log, int64_t log_cap, void* ev_before,
+                           void* ev_after, void* stream) {
     if (!shape_ok(shape) || Tin == Tout || nranks < 1) return (int)hipErrorInvalidValue;
     if (ev_before) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_before), S(stream));
     const int err = launch_update_mode<kShardFused>(Tin, Tout, *shape, parity & 1, ctl, parts,
                                                     log, nullptr, log_cap, recv, 0, nranks,
-                                                    S(stream));
+                                                    S(stream), 0,
+                                                    folds_pack(*shape) ? send : nullptr);
     if (ev_after) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_after), S(stream));
     return err;
+}
+
+int smx_shard_folds_pack(const smx_shape* shape) {
+    return shape_ok(shape) && folds_pack(*shape) ? 1 : 0;
 }
 
 int smx_shard_ahead(const double* T, const smx_shape* shape, int32_t parity, const double* recv,

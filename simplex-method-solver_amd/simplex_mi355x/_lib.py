@@ -25,7 +25,7 @@ PART_BYTES = 32
 CTL_DTYPE = np.dtype([
     ("negb", "<i4", (2,)), ("negf", "<i4", (2,)), ("term", "<i4"), ("sel_status", "<i4"),
     ("sel_r", "<i4"), ("sel_c", "<i4"), ("sel_e", "<f8"), ("npivots", "<i8"),
-    ("sel_owner", "<i4"), ("pad0", "<i4"), ("shard_off", "<i8"), ("xpos", "<i4", (2, 2)),
+    ("sel_owner", "<i4"), ("nla", "<i4"), ("shard_off", "<i8"), ("xpos", "<i4", (2, 2)),
     ("npiv", "<i8", (2,)), ("dec", "<i4", (2, 4)),
 ])
 ABSENT = -0x80000000
@@ -49,7 +49,7 @@ EXPORTS = (
     "smx_shard_run", "smx_shard_run_timed", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
     "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
     "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
-    "smx_copy_probe",
+    "smx_copy_probe", "smx_shard_folds_pack",
 )
 
 
@@ -104,12 +104,13 @@ def load():
         "smx_shard_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp, vp, vp], ctypes.c_int),
         "smx_shard_fused_prime": ([vp, sp, i32, vp, vp, vp], ctypes.c_int),
         "smx_shard_fused_begin": ([vp, sp, i32, vp, vp, vp, vp], ctypes.c_int),
-        "smx_shard_fused_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, vp, i64, vp, vp, vp],
+        "smx_shard_fused_finish": ([vp, vp, vp, i32, sp, i32, vp, vp, vp, vp, i64, vp, vp, vp],
                                    ctypes.c_int),
         "smx_fused_publish": ([sp, i32, vp, vp, vp], ctypes.c_int),
         "smx_shard_ahead": ([vp, sp, i32, vp, i32, vp, vp, vp, vp], ctypes.c_int),
         "smx_shard_sweep": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_copy_probe": ([vp, vp, i64, i32, vp], ctypes.c_int),
+        "smx_shard_folds_pack": ([sp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -101,8 +101,8 @@ class HipShardBackend:
         L = _lib.load()
         if self.fused:
             p = d.step & 1
-            if self.overlap and self._packed:
-                return          # packed by the previous finish (smx_shard_ahead)
+            if self._packed:
+                return          # packed by the previous finish (fused update / shard_ahead)
             if not self._records:
                 _lib.check(L.smx_shard_fused_prime(
                     d.buf[p].data_ptr(), ctypes.byref(self._shape), p, d.ctl.data_ptr(),
@@ -142,13 +142,15 @@ class HipShardBackend:
             d._pending = True
             return
         if self.fused:
+            # the update's last look-ahead workgroup also packs the next step into send
             _lib.check(_lib.load().smx_shard_fused_finish(
                 d.buf[p].data_ptr(), d.buf[p ^ 1].data_ptr(), self.recv.data_ptr(), self.world,
                 ctypes.byref(self._shape), p, d.ctl.data_ptr(), d.parts.data_ptr(),
-                d.log.data_ptr(), d.log_cap,
+                self.send.data_ptr(), d.log.data_ptr(), d.log_cap,
                 ev_before.cuda_event if ev_before is not None else None,
                 ev_after.cuda_event if ev_after is not None else None, d.stream.cuda_stream),
                 "smx_shard_fused_finish")
+            self._packed = bool(_lib.load().smx_shard_folds_pack(ctypes.byref(self._shape)))
             d.step += 1
             d._pending = True
             return

@@ -63,6 +63,8 @@ def _simulate(T, n, m, k, P, mode="overlap", bes=None):
     ("uniform", 40, 30, 78, 3),   # step 26 pivots on row 26 = rank 2's first row: on rank 1
                                   # r - row0 == its f-row replica's local index (regression)
     ("mixed", 5, 7, 30, 8),       # fewer constraint rows than ranks: some ranks own none
+    ("uniform", 4095, 4095, 24, 2),   # >= 64 MiB per shard: the update packs the next step
+    ("mixed", 4096, 4095, 24, 2),
     ("degenerate_mixed", 9, 3, 40, 4),
 ])
 def test_hip_shards_match_oracle(kind, n, m, k, P, mode):
