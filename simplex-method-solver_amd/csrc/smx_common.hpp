@@ -1,0 +1,232 @@
+// smx_common.hpp -- constants, ratio-test order, wave reductions, the decision from partials and from gathered shard headers
+// Part of libsmx (compiled as one translation unit by smx_kernels.hip; not a standalone header).
+#pragma once
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kSelBlock = 256;
+constexpr int kUpdBlock = 256;
+constexpr int kUpdWaves = kUpdBlock / kWave;
+constexpr int kMaxParts = 64;
+
+
+// ---------------------------------------------------------------------------------------------
+// Ratio-test candidate order (simplex.py:105-141 restated as an arg-min, see oracle/numpy_oracle):
+// class 0: v < 0, larger v better, ties -> larger row; class 1: v == 0 (incl. -0.0), smaller row;
+// class 2: v > 0, smaller row; class 3: no candidate.  NaN ratios never enter this order.
+struct Cand {
+    int cls;
+    int idx;
+    double v;
+};
+
+__device__ __forceinline__ Cand cand_none() { return Cand{3, SMX_NONE, 0.0}; }
+
+__device__ __forceinline__ Cand classify(double v, int idx) {
+    Cand c;
+    c.cls = (v < 0.0) ? 0 : ((v == 0.0) ? 1 : 2);
+    c.idx = idx;
+    c.v = v;
+    return c;
+}
+
+__device__ __forceinline__ bool better(const Cand& a, const Cand& b) {
+    if (a.cls != b.cls) return a.cls < b.cls;
+    if (a.cls == 0) return (a.v > b.v) || (a.v == b.v && a.idx > b.idx);
+    return a.idx < b.idx;
+}
+
+__device__ __forceinline__ Cand shfl_xor_cand(const Cand& a, int mask) {
+    Cand o;
+    o.cls = __shfl_xor(a.cls, mask, kWave);
+    o.idx = __shfl_xor(a.idx, mask, kWave);
+    o.v = __shfl_xor(a.v, mask, kWave);
+    return o;
+}
+
+// "first candidate" = smallest row with T[i][c] != 0, carrying its (possibly NaN) ratio
+struct First {
+    int idx;
+    double v;
+};
+
+__device__ __forceinline__ First shfl_xor_first(const First& a, int mask) {
+    First o;
+    o.idx = __shfl_xor(a.idx, mask, kWave);
+    o.v = __shfl_xor(a.v, mask, kWave);
+    return o;
+}
+
+__device__ __forceinline__ int wave_min_int(int x) {
+#pragma unroll
+    for (int mask = 32; mask >= 1; mask >>= 1) x = min(x, __shfl_xor(x, mask, kWave));
+    return x;
+}
+
+__device__ __forceinline__ Cand wave_best(Cand a) {
+#pragma unroll
+    for (int mask = 32; mask >= 1; mask >>= 1) {
+        Cand o = shfl_xor_cand(a, mask);
+        if (better(o, a)) a = o;
+    }
+    return a;
+}
+
+__device__ __forceinline__ First wave_first(First a) {
+#pragma unroll
+    for (int mask = 32; mask >= 1; mask >>= 1) {
+        First o = shfl_xor_first(a, mask);
+        if (o.idx < a.idx) a = o;
+    }
+    return a;
+}
+
+struct Decision {
+    int status;
+    int r;
+    int c;
+};
+
+// The outcome of pick_element from the select partials (run by one wave; lanes cover parts).
+// simplex.py:72-91 (phase 1), :94-103 (entering column / optimum), :105-141 (leaving row).
+__device__ Decision decide_from_parts(const smx_ctl* ctl, const smx_part* parts, int nparts,
+                                      int parity, int n, int m, int flen) {
+    const int lane = threadIdx.x & (kWave - 1);
+    Decision d;
+    const int negb = ctl->negb[parity];
+    if (negb != SMX_NONE && negb < n) {
+        int p1 = SMX_NONE;
+        for (int k = lane; k < nparts; k += kWave) p1 = min(p1, parts[k].p1col);
+        p1 = wave_min_int(p1);
+        d.r = negb;
+        d.c = p1;
+        d.status = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
+        return d;
+    }
+    const int c = ctl->negf[parity];
+    d.c = c;
+    d.r = SMX_NONE;
+    if (c == SMX_NONE) {
+        d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
+        return d;
+    }
+    First f{SMX_NONE, 0.0};
+    Cand b = cand_none();
+    for (int k = lane; k < nparts; k += kWave) {
+        const smx_part p = parts[k];
+        if (p.first < f.idx) {
+            f.idx = p.first;
+            f.v = p.first_v;
+        }
+        Cand o{p.best_cls, p.best_i, p.best_v};
+        if (better(o, b)) b = o;
+    }
+    f = wave_first(f);
+    b = wave_best(b);
+    if (f.idx == SMX_NONE) {
+        d.status = SMX_NOT_CONVERGE;              // first_try still set (simplex.py:138)
+    } else if (isnan(f.v)) {
+        d.status = SMX_PIVOT;                     // a NaN first candidate sticks (:117-121)
+        d.r = f.idx;
+    } else if (b.cls >= 2) {
+        d.status = SMX_NOT_CONVERGE;              // min_val > 0 (simplex.py:138-139)
+    } else {
+        d.status = SMX_PIVOT;
+        d.r = b.idx;
+    }
+    return d;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Every rank merges the P headers identically: phase decision (simplex.py:72-76), global arg-min
+// of the ratio test (simplex.py:105-141) and the winning row's offset in recv.  One thread.
+struct ShardDecision {
+    int status, r, c, owner;
+    int64_t off;
+};
+
+__device__ ShardDecision merge_headers(const double* __restrict__ recv, int nranks, int64_t ld,
+                                       int m, int flen) {
+    const int64_t slot = SMX_SHARD_HDR + 2 * ld;
+    int gnegb = SMX_NONE, owner_b = -1;
+    int gfirst = SMX_NONE, owner_f = -1;
+    double fv = 0.0;
+    Cand best = cand_none();
+    int owner_best = -1;
+    int c = SMX_NONE;
+    for (int p = 0; p < nranks; ++p) {
+        const double* h = recv + p * slot;
+        const int nb = (int)h[0];
+        if (nb < gnegb) {
+            gnegb = nb;
+            owner_b = p;
+        }
+        const int fi = (int)h[1];
+        if (fi < gfirst) {
+            gfirst = fi;
+            fv = h[2];
+            owner_f = p;
+        }
+        Cand o{(int)h[3], (int)h[4], h[5]};
+        if (better(o, best)) {
+            best = o;
+            owner_best = p;
+        }
+        c = (int)h[6];
+    }
+    ShardDecision d{SMX_NOT_CONVERGE, SMX_NONE, c, -1, 0};
+    if (gnegb != SMX_NONE) {                      // phase 1: the owner scanned its row
+        d.r = gnegb;
+        d.owner = owner_b;
+        d.off = owner_b * slot + SMX_SHARD_HDR + ld;
+        d.c = (int)recv[owner_b * slot + 7];
+        d.status = (d.c == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
+    } else if (c == SMX_NONE) {
+        d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;
+    } else if (gfirst == SMX_NONE) {
+        d.status = SMX_NOT_CONVERGE;
+    } else if (isnan(fv)) {
+        d.status = SMX_PIVOT;
+        d.r = gfirst;
+        d.owner = owner_f;
+        d.off = owner_f * slot + SMX_SHARD_HDR;
+    } else if (best.cls >= 2) {
+        d.status = SMX_NOT_CONVERGE;
+    } else {
+        d.status = SMX_PIVOT;
+        d.r = best.idx;
+        d.owner = owner_best;
+        d.off = owner_best * slot + SMX_SHARD_HDR + ld;
+    }
+    return d;
+}
+
+// commit = false: record the selection only (smx_shard_merge, like k_finalize); commit = true:
+// also count/log the pivot or latch the terminal outcome (the update kernel's block 0).
+__device__ void publish_shard_decision(const ShardDecision& d, const double* recv,
+                                       smx_ctl* ctl, int32_t* log, int64_t log_cap, bool commit) {
+    ctl->sel_status = d.status;
+    ctl->sel_r = d.r;
+    ctl->sel_c = d.c;
+    ctl->sel_owner = d.owner;
+    ctl->shard_off = d.off;
+    ctl->sel_e = (d.status == SMX_PIVOT) ? recv[d.off + d.c] : 0.0;
+    if (!commit) return;
+    if (d.status == SMX_PIVOT) {
+        const int64_t k = ctl->npivots;   // sharded: only block 0 of the update reads/writes it
+        if (log_cap > 0) {
+            log[2 * (k % log_cap)] = d.r;
+            log[2 * (k % log_cap) + 1] = d.c;
+        }
+        ctl->npivots = k + 1;
+    } else {
+        ctl->term = 1;
+    }
+}
+
+// Every rank merges the P headers identically (one workgroup) and, in phase 1, scans the
+// winning row for its first positive entry (simplex.py:81-85).
+
+}  // namespace

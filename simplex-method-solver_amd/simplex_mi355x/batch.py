@@ -3,7 +3,7 @@
 The reference UI solves 2-variable LPs with a handful of constraints (main.py:309-313); on the
 GPU one such solve is pure launch latency.  ``solve_batch`` packs up to millions of small problems
 (n <= 63 constraints, m + 1 <= 64 columns) and runs each one's whole pivot loop inside one
-wavefront of ``k_batch`` (csrc/smx_kernels.hip).  Per problem the result is exactly what
+wavefront of ``k_batch`` (csrc/smx_batch.hpp).  Per problem the result is exactly what
 ``SimplexMethod(constraints, function).get_solution()`` returns (simplex.py:179-199): the list of
 ``Info`` snapshots (labels, table, i/j, x1/x2/optimum) with the trailing ``Error`` on the two
 ``ValueError`` outcomes.  Problems outside the batch kernel's envelope (bigger, ragged, or with a
