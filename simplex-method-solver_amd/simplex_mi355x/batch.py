@@ -149,27 +149,40 @@ def _table(T, n, flen, m):
     return rows
 
 
+def _tables(S, n, flen, m):
+    """All snapshots of one LP as Python lists in one conversion (f-row cut to len(function))."""
+    tabs = S[:, :n + 1, :m + 1].tolist()
+    if flen < m + 1:
+        for t in tabs:
+            t[n] = t[n][:flen]
+    return tabs
+
+
 def _assemble(problem, dims, final, rc, xv, snaps, status, np_, P):
     """Build the get_solution list (simplex.py:179-199) from the device outputs."""
     cons, func = problem
     n, m, flen = (int(v) for v in dims)
     row, col = _labels(n, m)
-    f = lambda x1, x2: func[0] * x1 + func[1] * x2          # simplex.py:48-49
-    first_table = [list(r) for r in cons] + [func]
-    res = [Info(row, col, first_table, None, None, 0, 0, 0)]
+    f0, f1 = func[0], func[1]                                # simplex.py:48-49
+    # snapshot #0 keeps the caller's values and types (simplex.py:181); rows of numbers, so a
+    # row-wise copy is the deep copy
+    res = [Info.owning(row, col, [list(r) for r in cons] + [list(func)], None, None, 0, 0, 0)]
+    rcl = rc[:np_].tolist()
+    xvl = xv[:np_].tolist()
+    tables = _tables(snaps[:np_], n, flen, m) if snaps is not None else None
     x1 = x2 = 0
     for s in range(np_):
-        r, c = int(rc[s, 0]), int(rc[s, 1])
-        if snaps is not None or s == 0:
+        r, c = rcl[s]
+        if tables is not None or s == 0:
             res[-1].i, res[-1].j = r, c                      # simplex.py:194-195
         row[c], col[r] = col[r], row[c]                      # simplex.py:152
-        x1 = float(xv[s, 0]) if 'x1' in col else 0           # simplex.py:51-68
-        x2 = float(xv[s, 1]) if 'x2' in col else 0
-        if snaps is not None:
-            res.append(Info(row, col, _table(snaps[s], n, flen, m), None, None, x1, x2,
-                            f(x1, x2)))
-    if snaps is None:   # like SimplexMethod.solve(record_history=False): initial + final
-        res.append(Info(row, col, _table(final, n, flen, m), None, None, x1, x2, f(x1, x2)))
+        x1 = xvl[s][0] if 'x1' in col else 0                 # simplex.py:51-68
+        x2 = xvl[s][1] if 'x2' in col else 0
+        if tables is not None:
+            res.append(Info.owning(row, col, tables[s], None, None, x1, x2, f0 * x1 + f1 * x2))
+    if tables is None:  # like SimplexMethod.solve(record_history=False): initial + final
+        res.append(Info.owning(row, col, _table(final, n, flen, m), None, None, x1, x2,
+                               f0 * x1 + f1 * x2))
     if status == _lib.OPTIMUM:
         return res, "optimum"
     if status in MESSAGES:

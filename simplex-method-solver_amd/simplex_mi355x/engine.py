@@ -55,6 +55,22 @@ class Info:
         self.x2 = x2
         self.optimum = optimum
 
+    @classmethod
+    def owning(cls, row, column, table, i, j, x1, x2, optimum):
+        """The same snapshot for a table the caller just built and hands over (fresh lists of
+        Python floats from the device download): labels are copied, the table is not
+        deep-copied again -- the observable object is identical."""
+        self = cls.__new__(cls)
+        self.row = row.copy()
+        self.column = column.copy()
+        self.table = table
+        self.i = i
+        self.j = j
+        self.x1 = x1
+        self.x2 = x2
+        self.optimum = optimum
+        return self
+
 
 class LazyInfo(Info):
     """An ``Info`` whose ``table`` is materialised on first access from the device history
@@ -223,6 +239,14 @@ class SimplexMethod:
         rows.append(T[self.n, :min(self.flen, self.m + 1)].tolist())
         return rows
 
+    def _snapshot(self, x1, x2, optimum) -> Info:
+        """Info of the current state (simplex.py:181, :197-198).  A downloaded table is a fresh
+        list of fresh floats, so it is handed over instead of deep-copied a second time; the
+        pristine table (the caller's own lists) is deep-copied like the reference does."""
+        if self._pristine:
+            return Info(self.row, self.column, self.table, None, None, x1, x2, optimum)
+        return Info.owning(self.row, self.column, self.table, None, None, x1, x2, optimum)
+
     @table.setter
     def table(self, value):
         cons, func = value[:-1], value[-1]
@@ -334,7 +358,7 @@ class SimplexMethod:
         if lazy and self.flen in (self.m, self.m + 1) and self.flen >= 2:
             return self._get_solution_lazy(max_pivots, detect_cycles, chunk)
         result = []
-        result.append(Info(self.row, self.column, self.table, None, None, 0, 0, 0))
+        result.append(self._snapshot(0, 0, 0))
         done = 0
         while True:
             try:
@@ -354,8 +378,7 @@ class SimplexMethod:
             self._apply(i, j)   # recalculate_matrix() without re-running the selection
             done += 1
             x1, x2 = self.find_optimum()
-            result.append(Info(self.row, self.column, self.table, None, None, x1, x2,
-                               self.f(x1, x2)))
+            result.append(self._snapshot(x1, x2, self.f(x1, x2)))
             if self._track(i, j, detect_cycles):
                 self.status = "cycle"
                 break
@@ -433,7 +456,7 @@ class SimplexMethod:
         if big:
             first = LazyInfo(self.row, self.column, hist, self.pivots, None, None, 0, 0, 0)
         else:
-            first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
+            first = self._snapshot(0, 0, 0)
         start = self.pivots
         budget = float("inf") if max_pivots is None else int(max_pivots)
         dev = self._dev
@@ -467,8 +490,7 @@ class SimplexMethod:
             out.append(LazyInfo(self.row, self.column, hist, self.pivots, None, None, x1, x2,
                                 self.f(x1, x2)))
         else:
-            out.append(Info(self.row, self.column, self.table, None, None, x1, x2,
-                            self.f(x1, x2)))
+            out.append(self._snapshot(x1, x2, self.f(x1, x2)))
         if status is None:
             self.status = "cap"
         elif status == "cycle":
@@ -483,7 +505,7 @@ class SimplexMethod:
         return out
 
     def _solve_stepwise(self, max_pivots, detect_cycles=False):
-        first = Info(self.row, self.column, self.table, None, None, 0, 0, 0)
+        first = self._snapshot(0, 0, 0)
         out = [first]
         done = 0
         while max_pivots is None or done < max_pivots:
@@ -491,8 +513,7 @@ class SimplexMethod:
                 ok, i, j, _ = self.pick_element()
             except ValueError as exc:
                 x1, x2 = self.find_optimum()
-                out.append(Info(self.row, self.column, self.table, None, None, x1, x2,
-                                self.f(x1, x2)))
+                out.append(self._snapshot(x1, x2, self.f(x1, x2)))
                 out.append(Error(str(exc)))
                 self.status = "error"
                 return out
@@ -509,5 +530,5 @@ class SimplexMethod:
         else:
             self.status = "optimum" if (max_pivots is None or done < max_pivots) else "cap"
         x1, x2 = self.find_optimum()
-        out.append(Info(self.row, self.column, self.table, None, None, x1, x2, self.f(x1, x2)))
+        out.append(self._snapshot(x1, x2, self.f(x1, x2)))
         return out
