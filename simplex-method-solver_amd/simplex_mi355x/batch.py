@@ -12,6 +12,8 @@ wavefront of ``k_batch`` (csrc/smx_batch.hpp).  Per problem the result is exactl
 """
 from __future__ import annotations
 
+import gc
+
 import numpy as np
 import torch
 
@@ -59,7 +61,9 @@ def solve_batch_arrays(tabs: np.ndarray, dims: np.ndarray, max_pivots: int = 256
     0..m_k; ``dims``: int32 [B][3] = (n, m, len(function)) with every problem inside the kernel's
     envelope (see ``eligible``).  Returns numpy arrays: ``final`` (same layout as tabs),
     ``status`` (SMX_* codes; SMX_PIVOT = max_pivots reached), ``npivots``, ``rc`` [B][P][2],
-    ``xv`` [B][P][2] (x1, x2 after each pivot) and, with ``history``, ``snaps`` [B][P][Rmax][ldb].
+    ``xv`` [B][P][2] (x1, x2 after each pivot) and, with ``history``, ``snaps``
+    [sum(npivots)][Rmax][ldb] -- problem k's tables after each of its pivots are
+    ``snaps[snap_off[k]:snap_off[k + 1]]`` (compacted on the device before the copy back).
     """
     if not torch.cuda.is_available():
         raise RuntimeError("simplex_mi355x needs an MI355X (HIP device); there is no CPU path")
@@ -93,7 +97,9 @@ def solve_batch_arrays(tabs: np.ndarray, dims: np.ndarray, max_pivots: int = 256
                "xv": d_xv.cpu().numpy(), "status": d_st.cpu().numpy(),
                "npivots": d_np.cpu().numpy()}
         if history:
-            res["snaps"] = d_snaps.cpu().numpy()
+            steps = torch.arange(max(P, 1), device=dev)[None, :] < d_np[:, None]
+            res["snaps"] = d_snaps[steps].cpu().numpy()
+            res["snap_off"] = np.concatenate([[0], np.cumsum(res["npivots"], dtype=np.int64)])
     return res
 
 
@@ -135,11 +141,19 @@ def solve_batch(problems, max_pivots: int = 256, history: bool = True, device=No
     tabs, dims = pack([problems[k] for k in idx])
     out = solve_batch_arrays(tabs, dims, max_pivots, history, device)
     P = int(max_pivots)
-    for q, k in enumerate(idx):
-        results[k], statuses[k] = _assemble(
-            problems[k], dims[q], out["final"][q], out["rc"][q], out["xv"][q],
-            out["snaps"][q] if history else None, int(out["status"][q]),
-            int(out["npivots"][q]), P)
+    # Hundreds of thousands of fresh, acyclic lists: pause the cyclic collector while they are
+    # built, or its generational passes rescan the growing result set (5x slower at 20k LPs).
+    gc_was_on = gc.isenabled()
+    gc.disable()
+    try:
+        for q, k in enumerate(idx):
+            results[k], statuses[k] = _assemble(
+                problems[k], dims[q], out["final"][q], out["rc"][q], out["xv"][q],
+                out["snaps"][out["snap_off"][q]:out["snap_off"][q + 1]] if history else None,
+                int(out["status"][q]), int(out["npivots"][q]), P)
+    finally:
+        if gc_was_on:
+            gc.enable()
     return results, statuses
 
 
