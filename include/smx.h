@@ -126,6 +126,10 @@ int smx_select(const double* T, const smx_shape* shape, int32_t parity, smx_ctl*
  * publish of ctl->negb.  Records are double-buffered: `parts` must hold 2 * nparts of them.
  * smx_tune_fused(0) restores the select + update pair; returns the previous setting. */
 int smx_tune_fused(int32_t on);
+/* Smallest local tableau buffer (bytes) for which the sharded fused update packs the next step
+ * itself (smx_shard_folds_pack; default INT64_MAX = never, it measured slower); -1 keeps it;
+ * returns the previous value. */
+int64_t smx_tune_fold(int64_t min_bytes);
 
 /* pick_element, part 2: reduce the partials into ctl->sel_* (does not set term, logs nothing). */
 int smx_finalize(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
@@ -208,8 +212,8 @@ int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_
  * header and candidate rows from this step's look-ahead records (parts slot `parity`, written by
  * smx_shard_fused_prime for the first step of a sequence, by the previous fused finish after
  * that); smx_shard_fused_finish merges, updates and writes the next step's records -- and, when
- * `send` is not NULL and smx_shard_folds_pack(shape) (local buffer >= 64 MiB, where the sweep
- * hides it), already packs the next step into it: then skip the next begin.  Before switching
+ * `send` is not NULL and smx_shard_folds_pack(shape) (off by default, see smx_tune_fold),
+ * already packs the next step into it: then skip the next begin.  Before switching
  * back to the unfused calls, smx_fused_publish(next parity) restores ctl->negb. */
 int smx_shard_folds_pack(const smx_shape* shape);
 int smx_shard_fused_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,

@@ -125,12 +125,14 @@ int g_variant = -1;       // smx_tune_set overrides
 constexpr int kLargeVariant = 1, kSmallVariant = 0;
 constexpr int64_t kCacheTable = 16ll << 20;
 constexpr int64_t kLaSweepTable = 256ll << 20;
-// Sharded fused update: its last look-ahead workgroup packs the next step (one workgroup reading
-// two rows) only when the local sweep is long enough to hide that (2048^2 world 1: 27.2 vs
-// 19.0 us per update; 16384^2 world 1: 812 us either way); smaller shards use k_pack<true>.
-constexpr int64_t kFoldPackTable = 64ll << 20;
+// Sharded fused update: its last look-ahead workgroup can pack the next step itself (pivot =
+// update + all-gather).  Off by default: measured at world size 1 (tools/fold_ab.py,
+// profiles/r01_fold_ab.jsonl) it adds ~40 us per pivot at the 4- and 8-GPU per-rank shapes
+// (4097 / 2049 x 16384: that workgroup's share of the sweep starts late and per-wave throughput
+// is latency-bound) and gains nothing at 16384^2; the separate k_pack<true> wins everywhere.
+int64_t g_fold_min_bytes = INT64_MAX;   // smx_tune_fold
 inline bool folds_pack(const smx_shape& s) {
-    return (int64_t)(s.rows + 1) * s.ld * 8 >= kFoldPackTable;
+    return (int64_t)(s.rows + 1) * s.ld * 8 >= g_fold_min_bytes;
 }
 int g_blocks_per_cu = 0;  // 0: kDefaultBpc, capped by the occupancy API (see blocks_per_cu)
 constexpr int kDefaultBpc = 5;
@@ -322,6 +324,12 @@ int smx_tune_set(int32_t variant, int32_t blocks_per_cu_override) {
     if (variant >= 0 || variant == -2) g_variant = variant >= 0 ? variant : -1;
     if (blocks_per_cu_override >= 0) g_blocks_per_cu = blocks_per_cu_override;
     return 0;
+}
+
+int64_t smx_tune_fold(int64_t min_bytes) {
+    const int64_t prev = g_fold_min_bytes;
+    if (min_bytes >= 0) g_fold_min_bytes = min_bytes;
+    return prev;
 }
 
 int smx_tune_fused(int32_t on) {

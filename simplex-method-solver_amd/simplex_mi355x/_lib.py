@@ -49,7 +49,7 @@ EXPORTS = (
     "smx_shard_run", "smx_shard_run_timed", "smx_shard_pack", "smx_shard_merge", "smx_shard_update", "smx_shard_begin",
     "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
     "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
-    "smx_copy_probe", "smx_shard_folds_pack",
+    "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
 )
 
 
@@ -111,6 +111,7 @@ def load():
         "smx_shard_sweep": ([vp, vp, vp, i32, sp, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_copy_probe": ([vp, vp, i64, i32, vp], ctypes.c_int),
         "smx_shard_folds_pack": ([sp], ctypes.c_int),
+        "smx_tune_fold": ([i64], ctypes.c_int64),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -21,6 +21,7 @@ passes rectangular float rows and ``len(function) == m``):
 from __future__ import annotations
 
 import copy
+import gc
 
 import numpy as np
 
@@ -357,6 +358,17 @@ class SimplexMethod:
             lazy = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS
         if lazy and self.flen in (self.m, self.m + 1) and self.flen >= 2:
             return self._get_solution_lazy(max_pivots, detect_cycles, chunk)
+        # every snapshot is a fresh acyclic list of lists: pause the cyclic collector so its
+        # passes do not rescan the growing history (the reference pays that; the result is equal)
+        gc_was_on = gc.isenabled()
+        gc.disable()
+        try:
+            return self._get_solution_eager(max_pivots, detect_cycles)
+        finally:
+            if gc_was_on:
+                gc.enable()
+
+    def _get_solution_eager(self, max_pivots, detect_cycles):
         result = []
         result.append(self._snapshot(0, 0, 0))
         done = 0

@@ -14,7 +14,7 @@ HEADER = os.path.join(REPO, "include", "smx.h")
 
 def _declared():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^int (smx_[a-z_]+)\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^int(?:64_t)? (smx_[a-z_]+)\(", text, flags=re.M)))
 
 
 def test_header_declares_the_path():

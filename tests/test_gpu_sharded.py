@@ -63,8 +63,7 @@ def _simulate(T, n, m, k, P, mode="overlap", bes=None):
     ("uniform", 40, 30, 78, 3),   # step 26 pivots on row 26 = rank 2's first row: on rank 1
                                   # r - row0 == its f-row replica's local index (regression)
     ("mixed", 5, 7, 30, 8),       # fewer constraint rows than ranks: some ranks own none
-    ("uniform", 4095, 4095, 24, 2),   # >= 64 MiB per shard: the update packs the next step
-    ("mixed", 4096, 4095, 24, 2),
+    ("uniform", 4095, 4095, 24, 2),   # 64 MiB per shard
     ("degenerate_mixed", 9, 3, 40, 4),
 ])
 def test_hip_shards_match_oracle(kind, n, m, k, P, mode):
@@ -163,3 +162,24 @@ def test_hip_shards_nan_first_candidate(mode, case, P):
     assert np.array_equal(np.nan_to_num(full[:n]).view(np.int64),
                           np.nan_to_num(Tref[:n]).view(np.int64))
     assert np.array_equal(np.isnan(full[:n]), np.isnan(Tref[:n]))
+
+
+@pytest.mark.parametrize("kind,n", [("uniform", 4095), ("mixed", 4096)])
+def test_hip_shards_folded_pack(kind, n):
+    """smx_tune_fold(0): the fused update's last look-ahead workgroup packs the next step."""
+    from oracle import c_oracle
+    from simplex_mi355x import _lib, lp
+    L = _lib.load()
+    m, k, P = 4095, 24, 2
+    prev = L.smx_tune_fold(0)
+    try:
+        T = lp.dense_tableau(kind, 7, n, m)
+        states, logs, tables, full, bes = _simulate(T, n, m, k, P, "fused")
+        assert all(L.smx_shard_folds_pack(__import__("ctypes").byref(b._shape)) for b in bes)
+    finally:
+        L.smx_tune_fold(prev)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    for s_, lg in zip(states, logs):
+        assert s_["npivots"] == done
+        assert np.array_equal(lg, log)
+    assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))

@@ -21,7 +21,7 @@ dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
 ok = True
 cases = (("uniform", 1023, 777, 120), ("mixed", 600, 500, 150),
          ("degenerate", 300, 300, 100), ("uniform", 40, 30, 400),
-         ("mixed", 4095, 4095, 40))   # >= 64 MiB shard: the update packs the next step
+         ("mixed", 4095, 4095, 40))
 modes = (("overlap", True, True), ("fused", True, False), ("unfused", False, False))
 for (mode, fused, overlap), (kind, n, m, k) in [(md, c) for md in modes for c in cases]:
     T = lp.dense_tableau(kind, 5, n, m)
