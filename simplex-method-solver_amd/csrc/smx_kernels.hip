@@ -576,10 +576,10 @@ int smx_comm_destroy(void* comm) {
 }
 
 namespace {
-// Fused sharded chain, per pivot: one ncclAllGather -> k_update<kShardFused> (merge, sweep, the
-// records of step k+1, and -- by its last look-ahead workgroup -- step k+1's header and candidate
-// rows in `send`).  Primed by k_la_prime + k_pack<true>, closed by k_publish.  e_upd: 2k events
-// around the updates.
+// Fused sharded chain, per pivot: k_pack<true> (step k's records -> header + candidate rows)
+// -> one ncclAllGather -> k_update<kShardFused> (merge, sweep, step k+1's records; with
+// smx_tune_fold also step k+1's pack, then the next k_pack is skipped).  Primed by k_la_prime,
+// closed by k_publish.  e_upd: 2k events around the updates.
 int shard_chain_fused(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
                       smx_ctl* ctl, smx_part* parts, double* send, double* recv, int nranks,
                       ncclComm_t comm, int32_t* log, int64_t log_cap, hipEvent_t* e_upd,

@@ -126,6 +126,8 @@ def _oracle_run(T, n, m, flen, k):
     ("mixed", 1023, 1023, 400, 100),      # phase 1 first
     ("degenerate", 511, 511, 300, 100),   # degenerate, zero ratios
     ("degenerate_mixed", 600, 300, 300, 100),
+    ("uniform", 65535, 255, 60, 30),      # very tall: 65536 rows x 256 columns
+    ("mixed", 255, 65535, 60, 30),        # very wide: 512 chunks per row, phase 1
 ])
 def test_fast_path_vs_oracle(kind, n, m, k, chunk):
     from simplex_mi355x import lp
