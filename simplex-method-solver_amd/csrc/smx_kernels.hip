@@ -334,7 +334,7 @@ int64_t smx_tune_fold(int64_t min_bytes) {
 
 int smx_tune_fused(int32_t on) {
     const int prev = g_fused;
-    if (on >= 0) g_fused = on > 2 ? 2 : on;
+    if (on >= 0) g_fused = on > 3 ? 3 : on;
     return prev;
 }
 
@@ -635,6 +635,8 @@ int launch_sweep(const double* Tin, double* Tout, const smx_shape& s, int parity
 struct Overlap {
     hipStream_t s2 = nullptr;
     hipEvent_t ev_sweep = nullptr, ev_gather = nullptr;
+    uint64_t* sig[2] = {nullptr, nullptr};   // signal memory: sweeps done, gathers done
+    uint64_t seq = 0;                        // next base of the (monotonic) counters
 };
 
 int overlap_for_device(Overlap** out) {
@@ -666,10 +668,20 @@ constexpr int kOverlapParts = 16;   // look-ahead workgroups of the overlapped c
 int shard_chain_overlap(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
                         smx_ctl* ctl, smx_part* parts, double* send, double* recv, int nranks,
                         ncclComm_t comm, int32_t* log, int64_t log_cap, hipEvent_t* e_upd,
-                        hipStream_t st) {
+                        hipStream_t st, bool values) {
     Overlap* o = nullptr;
     int err = overlap_for_device(&o);
     if (err) return err;
+    for (int q = 0; values && q < 2 && !o->sig[q]; ++q) {   // one 8-B signal each, zeroed
+        hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&o->sig[q]),
+                                             sizeof(uint64_t), hipMallocSignalMemory);
+        if (e == hipSuccess) e = hipStreamWriteValue64(st, o->sig[q], 0, 0);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            o->sig[q] = nullptr;
+            return (int)e;
+        }
+    }
     smx_shape sx = s;
     sx.nparts = s.nparts < kOverlapParts ? s.nparts : kOverlapParts;
     const int npx = sx.nparts;
@@ -680,7 +692,14 @@ int shard_chain_overlap(double* buf0, double* buf1, const smx_shape& s, int pari
     if (!err) err = launch_pack<true>(T0, sx, parity, ctl, parts + (size_t)parity * npx, send, st);
     if (!err) err = nccl_err(ncclAllGather(send, recv + (size_t)parity * rsz, slot, ncclFloat64,
                                            comm, st));
-    if (!err) err = (int)hipEventRecord(o->ev_sweep, st);
+    // `values`: the two cross-stream dependencies as stream memory operations on monotonic
+    // counters (sig[0] = sweeps done + 1, sig[1] = gathers done) instead of events
+    const uint64_t base = o->seq;
+    auto signal_sweep = [&](uint64_t v) {
+        return values ? (int)hipStreamWriteValue64(st, o->sig[0], base + v, 0)
+                      : (int)hipEventRecord(o->ev_sweep, st);
+    };
+    if (!err) err = signal_sweep(1);
     for (int step = 0; step < k && !err; ++step) {
         const int p = (parity + step) & 1;
         double* tin = p ? buf1 : buf0;
@@ -688,18 +707,26 @@ int shard_chain_overlap(double* buf0, double* buf1, const smx_shape& s, int pari
         const double* rc = recv + (size_t)p * rsz;
         double* rn = recv + (size_t)(p ^ 1) * rsz;
         const bool more = step + 1 < k;
-        err = (int)hipStreamWaitEvent(o->s2, o->ev_sweep, 0);
+        err = values ? (int)hipStreamWaitValue64(o->s2, o->sig[0], base + step + 1,
+                                                 hipStreamWaitValueGte, ~0ull)
+                     : (int)hipStreamWaitEvent(o->s2, o->ev_sweep, 0);
         if (!err) err = launch_ahead(tin, sx, p, rc, nranks, ctl, parts, send, more, o->s2);
         if (!err && more)
             err = nccl_err(ncclAllGather(send, rn, slot, ncclFloat64, comm, o->s2));
-        if (!err) err = (int)hipEventRecord(o->ev_gather, o->s2);
+        if (!err)
+            err = values ? (int)hipStreamWriteValue64(o->s2, o->sig[1], base + step + 1, 0)
+                         : (int)hipEventRecord(o->ev_gather, o->s2);
         if (err) break;
         if (e_upd) (void)hipEventRecord(e_upd[2 * step], st);
         err = launch_sweep(tin, tout, s, p, rc, nranks, ctl, log, log_cap, npx, st);
         if (e_upd) (void)hipEventRecord(e_upd[2 * step + 1], st);
-        if (!err) err = (int)hipStreamWaitEvent(st, o->ev_gather, 0);
-        if (!err) err = (int)hipEventRecord(o->ev_sweep, st);
+        if (!err)
+            err = values ? (int)hipStreamWaitValue64(st, o->sig[1], base + step + 1,
+                                                     hipStreamWaitValueGte, ~0ull)
+                         : (int)hipStreamWaitEvent(st, o->ev_gather, 0);
+        if (!err) err = signal_sweep(step + 2);
     }
+    o->seq = base + k + 2;
     if (!err) err = launch_publish(sx, (parity + k) & 1, ctl, parts, st);
     return err;
 }
@@ -725,10 +752,10 @@ int smx_shard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
                   smx_ctl* ctl, smx_part* parts, double* send, double* recv, int32_t nranks,
                   void* comm, int32_t* log, int64_t log_cap, void* stream) {
     if (!shape_ok(shape) || !comm || nranks < 1 || k < 0) return (int)hipErrorInvalidValue;
-    if (g_fused == 2 && k > 0)
+    if (g_fused >= 2 && k > 0)
         return shard_chain_overlap(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
                                    nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap,
-                                   nullptr, S(stream));
+                                   nullptr, S(stream), g_fused == 3);
     if (g_fused && k > 0)
         return shard_chain_fused(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
                                  nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap,
@@ -760,10 +787,10 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     }
     (void)hipEventRecord(ev[2 * k], st);
     int err = 0;
-    if (g_fused == 2)
+    if (g_fused >= 2)
         err = shard_chain_overlap(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
                                   nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap, ev,
-                                  st);
+                                  st, g_fused == 3);
     else if (g_fused)
         err = shard_chain_fused(buf0, buf1, *shape, parity & 1, k, ctl, parts, send, recv,
                                 nranks, reinterpret_cast<ncclComm_t>(comm), log, log_cap, ev, st);

@@ -89,7 +89,9 @@ class HipShardBackend:
             self.recv = self._recv2[:world * self.slot]
         self._shape = ops.make_shape(self.dev.shape)
         self.fused = _lib.fused_enabled() if fused is None else bool(fused)
-        self.overlap = bool(overlap) and self.fused
+        # True / "events": the exchange stream synchronised by events; "values": by stream
+        # memory operations on device counters
+        self.overlap = overlap if (overlap and self.fused) else False
         self._records = False   # look-ahead records of step dev.step are in dev.parts
         self._packed = False    # overlap form: send already holds step dev.step's pack
 
@@ -166,7 +168,8 @@ class HipShardBackend:
     def _chain_mode(self):
         """Run the native chain in this backend's mode (smx_tune_fused is process-wide)."""
         L = _lib.load()
-        prev = L.smx_tune_fused((2 if self.overlap else 1) if self.fused else 0)
+        mode = (3 if self.overlap == "values" else 2) if self.overlap else 1
+        prev = L.smx_tune_fused(mode if self.fused else 0)
         return L, prev
 
     def run_native(self, k: int, comm: "RcclComm") -> None:

@@ -29,10 +29,16 @@ def main():
     dist.init_process_group("gloo")
     L = _lib.load()
     T = lp.dense_tableau("uniform", 0, n, m)
-    forms = (("fused+fold", True, 0), ("fused", True, 1 << 62), ("unfused", False, 1 << 62))
-    for name, fused, fold in forms:
+    off = 1 << 62
+    forms = (("fused+fold", True, 0, False), ("fused", True, off, False),
+             ("unfused", False, off, False), ("overlap-events", True, off, "events"),
+             ("overlap-values", True, off, "values"))
+    only = os.environ.get("FORMS")
+    for name, fused, fold, overlap in forms:
+        if only and name not in only.split(","):
+            continue
         L.smx_tune_fold(fold)
-        be = HipShardBackend(T, n, m, m, 0, 1, device="cuda:0", fused=fused)
+        be = HipShardBackend(T, n, m, m, 0, 1, device="cuda:0", fused=fused, overlap=overlap)
         comm = RcclComm()
         be.run_native(10, comm)
         torch.cuda.synchronize()
@@ -47,7 +53,7 @@ def main():
         comm.close()
         del be
         torch.cuda.empty_cache()
-    L.smx_tune_fold(64 << 20)
+    L.smx_tune_fold(off)
     dist.destroy_process_group()
 
 
