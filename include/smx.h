@@ -67,7 +67,7 @@ typedef struct smx_ctl {
     int32_t xpos[2][2]; /* [parity][x1, x2]: position code of labels 'x1', 'x2' (simplex.py:
                            58-59): p >= 0 row p (basic), -(j+1) column j, SMX_ABSENT none      */
     int64_t npiv[2];    /* [parity]: pivot index of the step (history ring position)          */
-    int32_t dec[2][4];  /* reserved (zero)                                                    */
+    int32_t dec[2][4];  /* dec[0][0]: smx_resident_run hand-off timeout flag; rest reserved   */
 } smx_ctl; /* 128 bytes */
 
 /* One per select workgroup (caller allocates 2 * nparts * sizeof(smx_part) bytes: the fused
@@ -263,6 +263,37 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
                         int32_t k, smx_ctl* ctl, smx_part* parts, double* send, double* recv,
                         int32_t nranks, void* comm, int32_t* log, int64_t log_cap, void* stream,
                         float* host_update_ms, float* host_total_ms);
+
+/* ---- on-chip resident pivot loop ---------------------------------------------------------
+ * The whole get_solution pivot loop (simplex.py:184-198) for k pivots in ONE persistent launch:
+ * G workgroups (one per CU, 1024 threads) each hold ceil(n/G) constraint rows and a replica of
+ * the f-row in LDS for the whole run and exchange one 32-B record ({payload, tag} granules) +
+ * one pivot row per pivot through `xch` (agent-coherent sc1 hand-offs, double-buffered).  Same decisions,
+ * same per-element arithmetic, same ctl / log / xhist bookkeeping and ping-pong convention as
+ * smx_run: the table after the d pivots actually applied is left in buf[(parity + d) & 1].
+ * Only unsharded tableaux whose rows fit in LDS (about R x C <= 2048^2, n <= 65534, C <= 4096)
+ * are eligible: smx_resident_bytes returns the `xch` size (0 when not eligible) and optionally
+ * plan_out[4] = {workgroups, rows per workgroup, elements per thread, LDS bytes}.
+ * `epoch` (1..4095) tags this launch's hand-offs: the caller zeroes `xch` when it allocates it,
+ * uses a different epoch for each of 4095 consecutive launches on it, and zeroes it again
+ * before an epoch value comes round again; k < 2^20 - 1.  A hand-off that does not complete
+ * within 2 s sets ctl->dec[0][0] = 1 and the kernel returns (the table is then undefined).
+ * smx_tune_resident: -1 never, 0 automatic, > 0 that many workgroups (<= 256), -2 keeps;
+ * returns the previous setting.
+ * smx_resident_trace (diagnostic): device buffer of 64 x G x 8 uint64 s_memrealtime stamps for
+ * steps from_step .. from_step+63 of later launches (NULL disables). */
+int smx_tune_resident(int32_t workgroups);
+int smx_resident_trace(void* trace, int32_t from_step);
+int64_t smx_resident_bytes(const smx_shape* shape, int32_t* plan_out);
+int smx_resident_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                     int32_t k, smx_ctl* ctl, void* xch, int64_t xch_bytes, int32_t epoch,
+                     int32_t* log, double* xhist, int64_t log_cap, void* stream);
+/* Self-check of the resident loop's division by the pivot element (the hardware division
+ * sequence with its denominator half hoisted, inside an exponent window) against the
+ * compiler's x / e on `count` device operand pairs: out[0] = pairs inside the window,
+ * out[1] = pairs whose results differ in any bit (device unsigned long long[2]). */
+int smx_fastdiv_check(const double* num, const double* den, int64_t count,
+                      unsigned long long* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,7 @@
 //   smx_update.hpp    k_update: recalculate_matrix (simplex.py:143-177), every mode
 //   smx_shard.hpp     row-sharded exchange kernels
 //   smx_batch.hpp     k_copy (copy-ceiling probe), k_batch (one small LP per wavefront)
+//   smx_resident.hpp  k_resident: the whole pivot loop in one persistent launch, tableau in LDS
 // and this file holds the host side: grid sizing, variants, chains, graphs, RCCL, the C ABI.
 //
 // Arithmetic parity: every element is (t*e - pr*pc)/e with each op rounded on its own, exactly
@@ -44,6 +45,7 @@ static_assert(sizeof(smx_part) == 32, "smx_part layout");
 #include "smx_update.hpp"
 #include "smx_shard.hpp"
 #include "smx_batch.hpp"
+#include "smx_resident.hpp"
 
 namespace {
 
@@ -291,6 +293,80 @@ int launch_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int
         if (err) return err;
     }
     return 0;
+}
+
+// ---- on-chip resident pivot loop (smx_resident.hpp) ------------------------------------------
+// -1: never; 0: automatic (one workgroup per CU, at most one per row); > 0: that many workgroups
+int g_resident = 0;
+uint64_t* g_resident_trace = nullptr;    // diagnostic stamps (smx_resident_trace)
+int g_resident_trace_from = 0;
+constexpr int64_t kResLdsMax = 160 * 1024 - 5 * 1024;   // dynamic LDS (static part ~4.2 KiB)
+constexpr int64_t kResLdsMin = 82 * 1024;               // > half a CU's LDS: one group per CU
+
+struct ResPlan {
+    int G, rpw, ept;
+    int64_t lds, rec_bytes, row_off, bytes;
+};
+
+bool resident_plan(const smx_shape& s, ResPlan* p) {
+    if (g_resident < 0) return false;
+    if (s.row0 != 0 || s.rows != s.n || s.n < 1 || s.m < 1 || s.n > kResMaxRows) return false;
+    if (s.m + 1 > 4096) return false;   // 13-bit phase-1 column in the record
+    const int C = s.m + 1;
+    // automatic: about four rows per workgroup (tools/resident_bench.py: 256^2 64 groups, 512^2
+    // 128, 1024^2 256), more when the rows do not fit in LDS, at most one workgroup per CU
+    const int64_t ldl = C | 1;
+    auto lds_of = [&](int r) { return ((int64_t)(r + 1) * ldl + C + (r + 1)) * 8; };
+    const int gmax = g_resident > 0 ? g_resident : (num_cus() < kResPollers ? num_cus() : kResPollers);
+    int G = g_resident > 0 ? g_resident : (s.n + 3) / 4;
+    if (G > gmax) G = gmax;
+    if (G > s.n) G = s.n;
+    int rpw = (s.n + G - 1) / G;
+    while (lds_of(rpw) > kResLdsMax && g_resident <= 0 && rpw > 1 && (s.n + rpw - 2) / (rpw - 1) <= gmax)
+        --rpw;
+    G = (s.n + rpw - 1) / rpw;              // no workgroup without rows
+    const int64_t lds = lds_of(rpw);
+    if (lds > kResLdsMax || G > kResPollers) return false;
+    p->G = G;
+    p->rpw = rpw;
+    p->ept = (int)(((int64_t)(rpw + 1) * C + kResBlock - 1) / kResBlock);
+    p->lds = lds < kResLdsMin ? kResLdsMin : lds;
+    p->rec_bytes = (int64_t)2 * G * kResRecWords * 8;
+    p->row_off = (p->rec_bytes + 255) / 256 * 256;
+    p->bytes = p->row_off + (int64_t)2 * G * 2 * s.ld * 8;
+    return true;
+}
+
+int launch_resident_kernel(double* buf0, double* buf1, const smx_shape& s, const ResPlan& p,
+                           int parity, int k, smx_ctl* ctl, char* xch, uint32_t epoch,
+                           int32_t* log, double* xhist, int64_t log_cap, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_resident,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kResLdsMax);
+        if (e != hipSuccess) return (int)e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_resident, dim3(p.G), dim3(kResBlock), (size_t)p.lds, st, buf0, buf1,
+                       s.ld, s.n, s.m, s.flen, fscan_of(s), parity, k, p.rpw, ctl, log, xhist,
+                       log_cap, reinterpret_cast<uint64_t*>(xch),
+                       reinterpret_cast<uint64_t*>(xch + p.row_off), s.ld, epoch,
+                       g_resident_trace, g_resident_trace_from);
+    return (int)hipGetLastError();
+}
+
+int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
+                    smx_ctl* ctl, void* xch, int64_t xch_bytes, uint32_t epoch, int32_t* log,
+                    double* xhist, int64_t log_cap, hipStream_t st) {
+    ResPlan p;
+    if (!resident_plan(s, &p) || xch == nullptr || xch_bytes < p.bytes || epoch < 1 ||
+        epoch > 4095 || k >= (1 << 20) - 1)
+        return (int)hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(&ctl->dec[0][0], 0, sizeof(int32_t), st);   // no latched timeout
+    if (e != hipSuccess) return (int)e;
+    return launch_resident_kernel(buf0, buf1, s, p, parity, k, ctl, static_cast<char*>(xch),
+                                  epoch, log, xhist, log_cap, st);
 }
 
 struct Graph {
@@ -891,6 +967,48 @@ int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_
                                      stream);
     if (ev_after) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_after), S(stream));
     return err;
+}
+
+int smx_tune_resident(int32_t workgroups) {
+    const int prev = g_resident;
+    if (workgroups >= -1) g_resident = workgroups > kResBlock ? kResBlock : workgroups;
+    return prev;
+}
+
+int smx_resident_trace(void* trace, int32_t from_step) {
+    g_resident_trace = static_cast<uint64_t*>(trace);
+    g_resident_trace_from = from_step < 0 ? 0 : from_step;
+    return 0;
+}
+
+int64_t smx_resident_bytes(const smx_shape* shape, int32_t* plan_out) {
+    ResPlan p;
+    if (!shape_ok(shape) || !resident_plan(*shape, &p)) return 0;
+    if (plan_out) {
+        plan_out[0] = p.G;
+        plan_out[1] = p.rpw;
+        plan_out[2] = p.ept;
+        plan_out[3] = (int32_t)p.lds;
+    }
+    return p.bytes;
+}
+
+int smx_resident_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                     int32_t k, smx_ctl* ctl, void* xch, int64_t xch_bytes, int32_t epoch,
+                     int32_t* log, double* xhist, int64_t log_cap, void* stream) {
+    if (!shape_ok(shape) || buf0 == buf1 || k < 0) return (int)hipErrorInvalidValue;
+    return launch_resident(buf0, buf1, *shape, parity & 1, k, ctl, xch, xch_bytes,
+                           (uint32_t)epoch, log, xhist, log_cap, S(stream));
+}
+
+int smx_fastdiv_check(const double* num, const double* den, int64_t count,
+                      unsigned long long* out, void* stream) {
+    if (count < 0 || !num || !den || !out) return (int)hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), S(stream));
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_fastdiv_check, dim3(1024), dim3(256), 0, S(stream), num, den, count,
+                       out);
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

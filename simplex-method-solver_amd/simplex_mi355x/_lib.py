@@ -50,6 +50,8 @@ EXPORTS = (
     "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
     "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
+    "smx_tune_resident", "smx_resident_trace", "smx_resident_bytes",
+    "smx_resident_run", "smx_fastdiv_check",
 )
 
 
@@ -112,6 +114,12 @@ def load():
         "smx_copy_probe": ([vp, vp, i64, i32, vp], ctypes.c_int),
         "smx_shard_folds_pack": ([sp], ctypes.c_int),
         "smx_tune_fold": ([i64], ctypes.c_int64),
+        "smx_tune_resident": ([i32], ctypes.c_int),
+        "smx_resident_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
+        "smx_resident_trace": ([vp, i32], ctypes.c_int),
+        "smx_resident_run": ([vp, vp, sp, i32, i32, vp, vp, i64, i32, vp, vp, i64, vp],
+                             ctypes.c_int),
+        "smx_fastdiv_check": ([vp, vp, i64, vp, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -125,6 +133,28 @@ def version() -> str:
     buf = ctypes.create_string_buffer(256)
     load().smx_version(buf, 256)
     return buf.value.decode()
+
+
+def resident_plan(shape) -> tuple[int, tuple[int, int, int, int]] | None:
+    """(exchange bytes, (workgroups, rows per workgroup, elements per thread, LDS bytes)) of the
+    on-chip resident pivot loop for ``shape`` = [ld, rows, n, m, flen, row0, nparts], or None
+    when the tableau is not eligible (sharded, or its rows do not fit in LDS)."""
+    sh = Shape(*(int(x) for x in shape))
+    plan = (ctypes.c_int32 * 4)()
+    nbytes = load().smx_resident_bytes(ctypes.byref(sh), plan)
+    if nbytes <= 0:
+        return None
+    return int(nbytes), tuple(int(x) for x in plan)
+
+
+def tune_resident(workgroups: int = -2) -> int:
+    """smx_tune_resident: -1 never, 0 automatic, > 0 that many workgroups, -2 query only;
+    returns the previous setting."""
+    return int(load().smx_tune_resident(workgroups))
+
+
+RESIDENT_TIMEOUT = 1   # smx_ctl.dec[0][0] after a resident hand-off timed out
+RESIDENT_EPOCHS = 4095   # tags of one exchange buffer cycle through epochs 1..4095
 
 
 def fused_enabled() -> bool:

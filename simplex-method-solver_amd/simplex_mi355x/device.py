@@ -12,6 +12,12 @@ Layout in HBM (one object per tableau, owned by torch tensors):
 * ``log``   : ``int32[log_cap][2]`` ring of applied pivots ``(r, c)``, drained by the host.
 * ``xhist`` : ``float64[log_cap][2]`` ring of ``(x1, x2)`` of the tableau after each pivot
   (find_optimum, simplex.py:51-68), written by the update kernel itself.
+* ``xch``   : exchange buffer of the on-chip resident loop (records + candidate rows), allocated
+  on first use for tableaux whose rows fit in LDS (``_lib.resident_plan``).
+
+Chained pivots run one of two ways: tableaux that fit on chip (about R x C <= 2048^2) run the
+whole chunk in ONE persistent launch that keeps the rows in LDS (``smx_resident_run``); larger
+ones replay a hipGraph of one fused update kernel per pivot (``smx_graph_*``).
 
 All launches go to one dedicated HIP stream per tableau; the host synchronises only when it
 reads the control block.
@@ -51,7 +57,8 @@ class DeviceTableau:
 
     def __init__(self, dense: np.ndarray, n: int, m: int, flen: int, *, device=None,
                  row0: int = 0, n_global: int | None = None, log_cap: int = 1 << 16,
-                 pad_to: int = 16, ld_extra: int = 0, defer_upload: bool = False):
+                 pad_to: int = 16, ld_extra: int = 0, defer_upload: bool = False,
+                 resident: bool | None = None):
         if not torch.cuda.is_available():
             raise RuntimeError("simplex_mi355x needs an MI355X (HIP device); there is no CPU path")
         _lib.load()
@@ -79,6 +86,10 @@ class DeviceTableau:
         self._pending = False   # chained pivots enqueued whose outcome the host has not read
         self._term = False      # a terminal outcome may be latched in ctl.term
         self._graphs: dict[tuple[int, int], Graph] = {}
+        # None: the library's policy (smx_tune_resident); False: always the launch chain
+        self.resident = resident
+        self._xch = None
+        self._epoch = 0
         if not defer_upload:
             self.upload(dense)
 
@@ -189,8 +200,13 @@ class DeviceTableau:
         if self._term:
             self.clear_term()
         p = self.step & 1
+        plan = self.resident_plan()
         with torch.cuda.stream(self.stream):
-            if graph:
+            if plan is not None:
+                xch, epoch = self._xch_for(plan), self._next_epoch()
+                ops.resident_run(self.buf, self.ctl, xch, self.log, self.xhist, self.shape, p,
+                                 k, epoch)
+            elif graph:
                 g = self._graphs.get((p, k))
                 if g is None:
                     g = self._make_graph(p, k)
@@ -202,10 +218,39 @@ class DeviceTableau:
         self.step += k
         self._pending = True
 
+    def resident_plan(self):
+        """The resident loop's (exchange bytes, (workgroups, rows per workgroup, columns per
+        thread, LDS bytes)) when :meth:`run` will use it, else None."""
+        if self.resident is False:
+            return None
+        return _lib.resident_plan(self.shape)
+
+    def _xch_for(self, plan) -> torch.Tensor:
+        nbytes = plan[0]
+        if self._xch is None or self._xch.numel() * 8 < nbytes:
+            with torch.cuda.stream(self.stream):
+                self._xch = torch.zeros((nbytes + 7) // 8, dtype=torch.int64, device=self.device)
+            self._epoch = 0
+        return self._xch
+
+    def _next_epoch(self) -> int:
+        """Tag of the next resident launch; the exchange buffer is re-zeroed when tags wrap."""
+        self._epoch += 1
+        if self._epoch > _lib.RESIDENT_EPOCHS:
+            with torch.cuda.stream(self.stream):
+                self._xch.zero_()
+            self._epoch = 1
+        return self._epoch
+
     def prepare(self, k: int) -> None:
-        """Capture (without running) the k-pivot graph the next ``run(k)`` will replay."""
+        """Capture (without running) the k-pivot graph the next ``run(k)`` will replay (or
+        allocate the resident loop's exchange buffer)."""
         self.settle()
         p = self.step & 1
+        plan = self.resident_plan()
+        if plan is not None:
+            self._xch_for(plan)
+            return
         if (p, k) not in self._graphs:
             with torch.cuda.stream(self.stream):
                 self._make_graph(p, k)
@@ -233,6 +278,10 @@ class DeviceTableau:
     def sync_state(self) -> np.void:
         """Read the control block and set the host step counter to the device pivot count."""
         c = self.read_ctl()
+        if int(c["dec"][0][0]) & _lib.RESIDENT_TIMEOUT:
+            self._pending = False
+            raise RuntimeError("resident pivot loop: a workgroup hand-off timed out (the "
+                               "tableau on the device is undefined)")
         self.step = int(c["npivots"])
         self._pending = False
         self._term = bool(c["term"])

@@ -133,6 +133,33 @@ def run(buf: Tensor, ctl: Tensor, parts: Tensor, log: Tensor, xhist: Tensor, sha
                                    _log_cap(log), _stream()), "smx_run")
 
 
+@torch.library.custom_op("smx::resident_run",
+                         mutates_args=("buf", "ctl", "xch", "log", "xhist"))
+def resident_run(buf: Tensor, ctl: Tensor, xch: Tensor, log: Tensor, xhist: Tensor,
+                 shape: list[int], parity: int, k: int, epoch: int) -> None:
+    """k pivots of the get_solution loop (simplex.py:184-198) in one persistent launch with the
+    tableau held in LDS (smx_resident_run); ``xch`` is the zero-initialised exchange buffer of
+    ``_lib.resident_plan(shape)[0]`` bytes and ``epoch`` (1..4095) tags this launch's
+    hand-offs (the caller rotates it and re-zeroes ``xch`` when it wraps)."""
+    if not 1 <= epoch <= _lib.RESIDENT_EPOCHS or not 0 <= k < (1 << 20) - 1:
+        raise ValueError(f"resident_run: epoch {epoch} / k {k} out of range")
+    if buf.dim() != 3 or buf.shape[0] != 2:
+        raise ValueError("buf must be (2, R, ld)")
+    _table_ok(buf[0], shape, "buf[0]")
+    _bytes_ok(ctl, _lib.CTL_BYTES, "ctl")
+    _xhist_ok(xhist, log)
+    plan = _lib.resident_plan(shape)
+    if plan is None:
+        raise ValueError(f"shape {list(shape)} is not eligible for the resident pivot loop")
+    _bytes_ok(xch, plan[0], "xch")
+    sh = make_shape(shape)
+    _lib.check(_lib.load().smx_resident_run(
+        _ptr(buf[0]), _ptr(buf[1]), ctypes.byref(sh), parity, k, _ptr(ctl), _ptr(xch),
+        xch.numel() * xch.element_size(), epoch, _ptr(log), _ptr(xhist), _log_cap(log),
+        _stream()),
+        "smx_resident_run")
+
+
 @torch.library.custom_op("smx::update_forced", mutates_args=("tout",))
 def update_forced(tin: Tensor, tout: Tensor, shape: list[int], r: int, c: int) -> None:
     """Forced pivot (r, c): the update kernel alone, for roofline measurement."""
