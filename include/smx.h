@@ -295,6 +295,36 @@ int smx_resident_run(double* buf0, double* buf1, const smx_shape* shape, int32_t
 int smx_fastdiv_check(const double* num, const double* den, int64_t count,
                       unsigned long long* out, void* stream);
 
+/* ---- block pivots: P pivots per HBM sweep ------------------------------------------------
+ * k pivots of the get_solution loop (simplex.py:184-198) in blocks of `pivots` (1..8): per block,
+ * `pivots` planning steps each decide one pivot (pick_element, simplex.py:70-141) from the block's
+ * input table T_k -- every value of T_{k+l} they need is re-derived from T_k with the update's own
+ * expression chained l times -- then ONE sweep applies all of them to every element
+ * (recalculate_matrix, simplex.py:143-177, the same operations in the same order per element),
+ * so a block moves 16*R*C bytes for `pivots` pivots.  Same decisions, bits, ctl / log / xhist
+ * bookkeeping and ping-pong convention as smx_run: the table after the d pivots actually applied
+ * is in buf[(parity + d) & 1] (the sweep works in place when a block applies an even count).
+ * Unsharded tableaux only (row0 = 0, rows = n).  `blk` is device scratch of smx_block_bytes
+ * bytes (no initialisation needed).  smx_block_bytes: with *pivots_inout = 0 it asks the
+ * library's policy (smx_tune_block: 0 automatic = 4 pivots for tables >= 64 MiB, 1 never, 2..8
+ * that many) and returns 0 when chains of `shape` would not use blocks; with 1..8 it asks for
+ * that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
+ * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
+ * entries) and the chain's total. */
+int smx_tune_block(int32_t pivots);
+int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout);
+int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                  int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log,
+                  double* xhist, int64_t log_cap, void* stream);
+int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                        int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                        int32_t* log, double* xhist, int64_t log_cap, void* stream,
+                        float* host_sweep_ms, float* host_total_ms);
+int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                           int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                           int32_t* log, double* xhist, int64_t log_cap, void* stream,
+                           void** graph_out);
+
 #ifdef __cplusplus
 }
 #endif

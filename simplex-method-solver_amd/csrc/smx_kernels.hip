@@ -9,6 +9,7 @@
 //   smx_shard.hpp     row-sharded exchange kernels
 //   smx_batch.hpp     k_copy (copy-ceiling probe), k_batch (one small LP per wavefront)
 //   smx_resident.hpp  k_resident: the whole pivot loop in one persistent launch, tableau in LDS
+//   smx_block.hpp     k_blk_*: P pivots per HBM sweep, decisions planned from the sweep's input
 // and this file holds the host side: grid sizing, variants, chains, graphs, RCCL, the C ABI.
 //
 // Arithmetic parity: every element is (t*e - pr*pc)/e with each op rounded on its own, exactly
@@ -46,6 +47,7 @@ static_assert(sizeof(smx_part) == 32, "smx_part layout");
 #include "smx_shard.hpp"
 #include "smx_batch.hpp"
 #include "smx_resident.hpp"
+#include "smx_block.hpp"
 
 namespace {
 
@@ -367,6 +369,127 @@ int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, 
     if (e != hipSuccess) return (int)e;
     return launch_resident_kernel(buf0, buf1, s, p, parity, k, ctl, static_cast<char*>(xch),
                                   epoch, log, xhist, log_cap, st);
+}
+
+// ---- block pivots (smx_block.hpp) ------------------------------------------------------------
+// smx_tune_block: 0 automatic, 1 never, 2..kBlkMax that many pivots per sweep
+int g_block = 0;
+constexpr int kBlockAutoP = 4;
+constexpr int64_t kBlockMinTable = 64ll << 20;
+
+int block_pivots(const smx_shape& s) {
+    if (g_block == 1) return 0;
+    if (s.row0 != 0 || s.rows != s.n || s.rows < 1 || s.m < 1) return 0;   // unsharded only
+    if (g_block >= 2) return g_block;
+    return (int64_t)(s.rows + 1) * s.ld * 8 >= kBlockMinTable ? kBlockAutoP : 0;
+}
+
+using BlkSweepFn = void (*)(double*, double*, int64_t, int, int, const BlkHdr*, const double*,
+                           const double*);
+using BlkColsFn = void (*)(const double*, int64_t, int, int, int, int, const smx_ctl*, char*,
+                           int64_t, int64_t, int64_t, double*, int64_t);
+using BlkDecFn = void (*)(const double*, int64_t, int, int, int, int, int, int, smx_ctl*, char*,
+                          int64_t, int64_t, int64_t, int64_t, int32_t*, double*, int64_t);
+
+template <bool NTL>
+BlkSweepFn blk_sweep_fn_ntl(int P) {
+    switch (P) {
+        case 1: return k_blk_sweep<1, NTL>;
+        case 2: return k_blk_sweep<2, NTL>;
+        case 3: return k_blk_sweep<3, NTL>;
+        case 4: return k_blk_sweep<4, NTL>;
+        case 5: return k_blk_sweep<5, NTL>;
+        case 6: return k_blk_sweep<6, NTL>;
+        case 7: return k_blk_sweep<7, NTL>;
+        default: return k_blk_sweep<8, NTL>;
+    }
+}
+
+BlkColsFn blk_cols_fn(int L) {
+    switch (L) {
+        case 0: return k_blk_cols<0>;
+        case 1: return k_blk_cols<1>;
+        case 2: return k_blk_cols<2>;
+        case 3: return k_blk_cols<3>;
+        case 4: return k_blk_cols<4>;
+        case 5: return k_blk_cols<5>;
+        case 6: return k_blk_cols<6>;
+        case 7: return k_blk_cols<7>;
+        default: return k_blk_cols<8>;
+    }
+}
+
+BlkDecFn blk_dec_fn(int L) {
+    switch (L) {
+        case 0: return k_blk_dec<0>;
+        case 1: return k_blk_dec<1>;
+        case 2: return k_blk_dec<2>;
+        case 3: return k_blk_dec<3>;
+        case 4: return k_blk_dec<4>;
+        case 5: return k_blk_dec<5>;
+        case 6: return k_blk_dec<6>;
+        default: return k_blk_dec<7>;
+    }
+}
+
+int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, char* blk,
+                       const BlkLayout& L, hipStream_t st) {
+    const bool ntl = (int64_t)(s.rows + 1) * s.ld * 8 > kCacheTable;
+    BlkSweepFn fn = ntl ? blk_sweep_fn_ntl<true>(P) : blk_sweep_fn_ntl<false>(P);
+    const int grid = update_grid(s, (const void*)fn, 0);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, tin, tother, s.ld, s.rows + 1,
+                       s.m + 1, reinterpret_cast<const BlkHdr*>(blk),
+                       reinterpret_cast<const double*>(blk + L.mul),
+                       reinterpret_cast<const double*>(blk + L.pr));
+    return (int)hipGetLastError();
+}
+
+// k pivots in blocks of P: prime, then per block P x (decide, columns) and one sweep; publish.
+// ev (optional): 2 events per block recorded around its sweep.
+int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, int P,
+                       smx_ctl* ctl, char* blk, int32_t* log, double* xhist, int64_t log_cap,
+                       hipStream_t st, hipEvent_t* ev = nullptr) {
+    const BlkLayout L = blk_layout(s.rows + 1, s.ld, s.nparts);
+    const int fscan = fscan_of(s);
+    const double* t0 = parity ? buf1 : buf0;
+    hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(kBlkDec), 0, st, t0, s.ld, s.rows, s.m, fscan,
+                       (const smx_ctl*)ctl, blk, L.fr);
+    hipLaunchKernelGGL(blk_cols_fn(0), dim3(s.nparts), dim3(kUpdBlock), 0, st, t0, s.ld, s.rows,
+                       s.m, P, parity, (const smx_ctl*)ctl, blk, L.parts, L.mul, L.pr, xhist,
+                       log_cap);
+    int err = (int)hipGetLastError();
+    int p = parity, done = 0, b = 0;
+    while (!err && done < k) {
+        const int Pb = (k - done < P) ? k - done : P;
+        double* tin = p ? buf1 : buf0;
+        double* toth = p ? buf0 : buf1;
+        for (int l = 0; l < Pb; ++l) {
+            hipLaunchKernelGGL(blk_dec_fn(l), dim3(1), dim3(kBlkDec), 0, st, (const double*)tin,
+                               s.ld, s.rows, s.m, s.flen, fscan, s.nparts, p, ctl, blk, L.parts,
+                               L.mul, L.pr, L.fr, log, xhist, log_cap);
+            hipLaunchKernelGGL(blk_cols_fn(l + 1), dim3(s.nparts), dim3(kUpdBlock), 0, st,
+                               (const double*)tin, s.ld, s.rows, s.m, Pb, p, (const smx_ctl*)ctl,
+                               blk, L.parts, L.mul, L.pr, xhist, log_cap);
+        }
+        err = (int)hipGetLastError();
+        if (ev) (void)hipEventRecord(ev[2 * b], st);
+        if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, L, st);
+        if (ev) (void)hipEventRecord(ev[2 * b + 1], st);
+        p = (p + Pb) & 1;
+        done += Pb;
+        ++b;
+    }
+    if (err) return err;
+    hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const char*)blk, L.parts,
+                       s.nparts, p, ctl);
+    return (int)hipGetLastError();
+}
+
+bool block_args_ok(const smx_shape* shape, int k, int P, const void* blk, int64_t blk_bytes) {
+    if (!shape_ok(shape) || k < 0 || P < 1 || P > kBlkMax || !blk) return false;
+    const smx_shape& s = *shape;
+    if (s.row0 != 0 || s.rows != s.n || s.rows < 1 || s.m < 1) return false;
+    return blk_bytes >= blk_layout(s.rows + 1, s.ld, s.nparts).bytes;
 }
 
 struct Graph {
@@ -1009,6 +1132,96 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
     hipLaunchKernelGGL(k_fastdiv_check, dim3(1024), dim3(256), 0, S(stream), num, den, count,
                        out);
     return (int)hipGetLastError();
+}
+
+int smx_tune_block(int32_t pivots) {
+    const int prev = g_block;
+    if (pivots >= 0) g_block = pivots > kBlkMax ? kBlkMax : pivots;
+    return prev;
+}
+
+int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout) {
+    if (!shape_ok(shape)) return 0;
+    const int req = pivots_inout ? *pivots_inout : 0;
+    if (req < 0 || req > kBlkMax) return 0;
+    const int P = req > 0 ? req : block_pivots(*shape);
+    if (P < 1 || !block_args_ok(shape, 0, P, shape, INT64_MAX)) return 0;
+    if (pivots_inout) *pivots_inout = P;
+    return blk_layout(shape->rows + 1, shape->ld, shape->nparts).bytes;
+}
+
+int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                  int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log,
+                  double* xhist, int64_t log_cap, void* stream) {
+    if (!block_args_ok(shape, k, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl)
+        return (int)hipErrorInvalidValue;
+    if (k == 0) return 0;
+    return launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                              static_cast<char*>(blk), log, xhist, log_cap, S(stream));
+}
+
+int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                        int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                        int32_t* log, double* xhist, int64_t log_cap, void* stream,
+                        float* host_sweep_ms, float* host_total_ms) {
+    if (!block_args_ok(shape, k, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || k < 1 ||
+        !host_sweep_ms || !host_total_ms)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    const int nb = (k + pivots - 1) / pivots;
+    hipEvent_t* ev = new hipEvent_t[2 * (size_t)nb + 2];
+    for (int i = 0; i < 2 * nb + 2; ++i) {
+        if (hipEventCreate(&ev[i]) != hipSuccess) {
+            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+            delete[] ev;
+            return (int)hipErrorOutOfMemory;
+        }
+    }
+    (void)hipEventRecord(ev[2 * nb], st);
+    int err = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                                 static_cast<char*>(blk), log, xhist, log_cap, st, ev);
+    (void)hipEventRecord(ev[2 * nb + 1], st);
+    if (!err) err = (int)hipEventSynchronize(ev[2 * nb + 1]);
+    if (!err) {
+        for (int b = 0; b < nb; ++b)
+            (void)hipEventElapsedTime(&host_sweep_ms[b], ev[2 * b], ev[2 * b + 1]);
+        (void)hipEventElapsedTime(host_total_ms, ev[2 * nb], ev[2 * nb + 1]);
+    }
+    for (int i = 0; i < 2 * nb + 2; ++i) (void)hipEventDestroy(ev[i]);
+    delete[] ev;
+    return err;
+}
+
+int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                           int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                           int32_t* log, double* xhist, int64_t log_cap, void* stream,
+                           void** graph_out) {
+    if (!block_args_ok(shape, k, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || k < 1 ||
+        !graph_out)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    Graph* g = new Graph();
+    hipError_t err = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+    if (err != hipSuccess) {
+        delete g;
+        return (int)err;
+    }
+    int lerr = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                                  static_cast<char*>(blk), log, xhist, log_cap, st);
+    err = hipStreamEndCapture(st, &g->graph);
+    if (lerr || err != hipSuccess) {
+        if (g->graph) (void)hipGraphDestroy(g->graph);
+        delete g;
+        return lerr ? lerr : (int)err;
+    }
+    err = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+    if (err != hipSuccess) {
+        (void)hipGraphDestroy(g->graph);
+        delete g;
+        return (int)err;
+    }
+    *graph_out = g;
+    return 0;
 }
 
 }  // extern "C"

@@ -52,6 +52,8 @@ EXPORTS = (
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
     "smx_tune_resident", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check",
+    "smx_tune_block", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
+    "smx_block_graph_create",
 )
 
 
@@ -120,6 +122,15 @@ def load():
         "smx_resident_run": ([vp, vp, sp, i32, i32, vp, vp, i64, i32, vp, vp, i64, vp],
                              ctypes.c_int),
         "smx_fastdiv_check": ([vp, vp, i64, vp, vp], ctypes.c_int),
+        "smx_tune_block": ([i32], ctypes.c_int),
+        "smx_block_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
+        "smx_block_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp],
+                          ctypes.c_int),
+        "smx_block_run_timed": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp,
+                                 ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)],
+                                ctypes.c_int),
+        "smx_block_graph_create": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp,
+                                    ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -151,6 +162,27 @@ def tune_resident(workgroups: int = -2) -> int:
     """smx_tune_resident: -1 never, 0 automatic, > 0 that many workgroups, -2 query only;
     returns the previous setting."""
     return int(load().smx_tune_resident(workgroups))
+
+
+def block_plan(shape, pivots: int = 0) -> tuple[int, int] | None:
+    """(scratch bytes, pivots per sweep) of the block-pivot chain for ``shape``: with
+    ``pivots`` = 0 under the library's policy (smx_tune_block; None when chains of this shape do
+    not use blocks), else for that many pivots per sweep (None when not eligible)."""
+    sh = Shape(*(int(x) for x in shape))
+    piv = ctypes.c_int32(int(pivots))
+    nbytes = load().smx_block_bytes(ctypes.byref(sh), ctypes.byref(piv))
+    if nbytes <= 0:
+        return None
+    return int(nbytes), int(piv.value)
+
+
+def tune_block(pivots: int = -1) -> int:
+    """smx_tune_block: 0 automatic, 1 never, 2..8 pivots per sweep, -1 query only; returns the
+    previous setting."""
+    return int(load().smx_tune_block(pivots))
+
+
+BLOCK_MAX = 8   # pivots per sweep at most
 
 
 RESIDENT_TIMEOUT = 1   # smx_ctl.dec[0][0] after a resident hand-off timed out

@@ -14,10 +14,14 @@ Layout in HBM (one object per tableau, owned by torch tensors):
   (find_optimum, simplex.py:51-68), written by the update kernel itself.
 * ``xch``   : exchange buffer of the on-chip resident loop (records + candidate rows), allocated
   on first use for tableaux whose rows fit in LDS (``_lib.resident_plan``).
+* ``blk``   : scratch of the block-pivot chain (pivot rows, per-row multipliers, records, the
+  running f-row), allocated on first use for tableaux it applies to (``_lib.block_plan``).
 
-Chained pivots run one of two ways: tableaux that fit on chip (about R x C <= 2048^2) run the
-whole chunk in ONE persistent launch that keeps the rows in LDS (``smx_resident_run``); larger
-ones replay a hipGraph of one fused update kernel per pivot (``smx_graph_*``).
+Chained pivots run one of three ways: tableaux that fit on chip (about R x C <= 2048^2) run the
+whole chunk in ONE persistent launch that keeps the rows in LDS (``smx_resident_run``); tables
+that stream from HBM (>= 64 MiB) replay a hipGraph of block pivots -- several pivots planned from
+the table, then applied in one sweep (``smx_block_graph_create``); the rest replay a hipGraph of
+one fused update kernel per pivot (``smx_graph_*``).
 
 All launches go to one dedicated HIP stream per tableau; the host synchronises only when it
 reads the control block.
@@ -58,7 +62,7 @@ class DeviceTableau:
     def __init__(self, dense: np.ndarray, n: int, m: int, flen: int, *, device=None,
                  row0: int = 0, n_global: int | None = None, log_cap: int = 1 << 16,
                  pad_to: int = 16, ld_extra: int = 0, defer_upload: bool = False,
-                 resident: bool | None = None):
+                 resident: bool | None = None, block: int | None = None):
         if not torch.cuda.is_available():
             raise RuntimeError("simplex_mi355x needs an MI355X (HIP device); there is no CPU path")
         _lib.load()
@@ -90,6 +94,9 @@ class DeviceTableau:
         self.resident = resident
         self._xch = None
         self._epoch = 0
+        # None: the library's policy (smx_tune_block); 0: never; 1..8: pivots per sweep
+        self.block = block
+        self._blk = None
         if not defer_upload:
             self.upload(dense)
 
@@ -201,11 +208,22 @@ class DeviceTableau:
             self.clear_term()
         p = self.step & 1
         plan = self.resident_plan()
+        bplan = self.block_plan() if plan is None else None
         with torch.cuda.stream(self.stream):
             if plan is not None:
                 xch, epoch = self._xch_for(plan), self._next_epoch()
                 ops.resident_run(self.buf, self.ctl, xch, self.log, self.xhist, self.shape, p,
                                  k, epoch)
+            elif bplan is not None:
+                blk = self._blk_for(bplan)
+                if graph:
+                    g = self._graphs.get((p, k, "blk", bplan[1]))
+                    if g is None:
+                        g = self._make_block_graph(p, k, bplan[1])
+                    g.launch(self.stream.cuda_stream)
+                else:
+                    ops.block_run(self.buf, self.ctl, blk, self.log, self.xhist, self.shape, p,
+                                  k, bplan[1])
             elif graph:
                 g = self._graphs.get((p, k))
                 if g is None:
@@ -224,6 +242,59 @@ class DeviceTableau:
         if self.resident is False:
             return None
         return _lib.resident_plan(self.shape)
+
+    def block_plan(self):
+        """(scratch bytes, pivots per sweep) of the block-pivot chain when :meth:`run` will use
+        it (the resident loop takes precedence), else None."""
+        if self.block == 0:
+            return None
+        return _lib.block_plan(self.shape, self.block or 0)
+
+    def _blk_for(self, plan) -> torch.Tensor:
+        nbytes = plan[0]
+        if self._blk is None or self._blk.numel() * 8 < nbytes:
+            with torch.cuda.stream(self.stream):
+                self._blk = torch.zeros((nbytes + 7) // 8, dtype=torch.int64, device=self.device)
+        return self._blk
+
+    def _make_block_graph(self, parity: int, k: int, pivots: int) -> Graph:
+        import ctypes
+        h = ctypes.c_void_p()
+        sh = ops.make_shape(self.shape)
+        blk = self._blk
+        _lib.check(_lib.load().smx_block_graph_create(
+            self.buf[0].data_ptr(), self.buf[1].data_ptr(), ctypes.byref(sh), parity, k, pivots,
+            self.ctl.data_ptr(), blk.data_ptr(), blk.numel() * 8, self.log.data_ptr(),
+            self.xhist.data_ptr(), self.log_cap, self.stream.cuda_stream, ctypes.byref(h)),
+            "smx_block_graph_create")
+        g = Graph(h.value)
+        self._graphs[(parity, k, "blk", pivots)] = g
+        return g
+
+    def run_block_timed(self, k: int, pivots: int):
+        """k chained pivots in blocks of ``pivots`` with HIP events around every sweep
+        (synchronous).  Returns (per-sweep ms array, device ms of the whole chain)."""
+        import ctypes
+        self.settle()
+        if self._term:
+            self.clear_term()
+        p = self.step & 1
+        nb = -(-k // pivots)
+        sw = (ctypes.c_float * nb)()
+        tot = ctypes.c_float()
+        plan = _lib.block_plan(self.shape, pivots)
+        if plan is None:
+            raise ValueError(f"shape {self.shape} is not eligible for block pivots")
+        blk = self._blk_for(plan)
+        sh = ops.make_shape(self.shape)
+        _lib.check(_lib.load().smx_block_run_timed(
+            self.buf[0].data_ptr(), self.buf[1].data_ptr(), ctypes.byref(sh), p, k, pivots,
+            self.ctl.data_ptr(), blk.data_ptr(), blk.numel() * 8, self.log.data_ptr(),
+            self.xhist.data_ptr(), self.log_cap, self.stream.cuda_stream, sw,
+            ctypes.byref(tot)), "smx_block_run_timed")
+        self.step += k
+        self._pending = True
+        return np.frombuffer(sw, dtype=np.float32).copy(), float(tot.value)
 
     def _xch_for(self, plan) -> torch.Tensor:
         nbytes = plan[0]
@@ -250,6 +321,13 @@ class DeviceTableau:
         plan = self.resident_plan()
         if plan is not None:
             self._xch_for(plan)
+            return
+        bplan = self.block_plan()
+        if bplan is not None:
+            self._blk_for(bplan)
+            if (p, k, "blk", bplan[1]) not in self._graphs:
+                with torch.cuda.stream(self.stream):
+                    self._make_block_graph(p, k, bplan[1])
             return
         if (p, k) not in self._graphs:
             with torch.cuda.stream(self.stream):

@@ -160,6 +160,26 @@ def resident_run(buf: Tensor, ctl: Tensor, xch: Tensor, log: Tensor, xhist: Tens
         "smx_resident_run")
 
 
+@torch.library.custom_op("smx::block_run", mutates_args=("buf", "ctl", "blk", "log", "xhist"))
+def block_run(buf: Tensor, ctl: Tensor, blk: Tensor, log: Tensor, xhist: Tensor,
+              shape: list[int], parity: int, k: int, pivots: int) -> None:
+    """k pivots of the get_solution loop (simplex.py:184-198) in blocks of ``pivots`` per HBM
+    sweep (smx_block_run): each block's decisions are planned from its input table, then one
+    sweep applies them all.  ``blk`` is scratch of ``_lib.block_plan(shape)[0]`` bytes."""
+    if not 1 <= pivots <= _lib.BLOCK_MAX or k < 0:
+        raise ValueError(f"block_run: pivots {pivots} / k {k} out of range")
+    if buf.dim() != 3 or buf.shape[0] != 2:
+        raise ValueError("buf must be (2, R, ld)")
+    _table_ok(buf[0], shape, "buf[0]")
+    _bytes_ok(ctl, _lib.CTL_BYTES, "ctl")
+    _xhist_ok(xhist, log)
+    sh = make_shape(shape)
+    _lib.check(_lib.load().smx_block_run(
+        _ptr(buf[0]), _ptr(buf[1]), ctypes.byref(sh), parity, k, pivots, _ptr(ctl), _ptr(blk),
+        blk.numel() * blk.element_size(), _ptr(log), _ptr(xhist), _log_cap(log), _stream()),
+        "smx_block_run")
+
+
 @torch.library.custom_op("smx::update_forced", mutates_args=("tout",))
 def update_forced(tin: Tensor, tout: Tensor, shape: list[int], r: int, c: int) -> None:
     """Forced pivot (r, c): the update kernel alone, for roofline measurement."""

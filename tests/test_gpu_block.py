@@ -1,0 +1,219 @@
+"""GPU parity of block pivots (smx_block_run, csrc/smx_block.hpp): P pivots planned from the
+block's input table and applied in one HBM sweep.  Bit-exact against the golden fixtures, the C
+oracle and the one-pivot-per-sweep chain, for every block size 1..8, ragged last blocks,
+terminal outcomes inside a block, the x-history ring and interleaving with host steps.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from golden_util import dec_input, load, table_hash, trajectory_cap, trajectory_cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+
+
+@pytest.fixture
+def block_mode():
+    """Set smx_tune_block for one test (resident loop off, so small tables take the block path)
+    and restore both policies afterwards."""
+    from simplex_mi355x import _lib
+    prev_b = _lib.tune_block(-1)
+    prev_r = _lib.tune_resident(-2)
+    _lib.tune_resident(-1)
+    yield _lib.tune_block
+    _lib.tune_block(prev_b)
+    _lib.tune_resident(prev_r)
+
+
+CASES = list(trajectory_cases())
+
+
+def _solve(cons, func, cap, chunk):
+    import simplex
+    sm = simplex.SimplexMethod([list(r) for r in cons], list(func))
+    out = sm.solve(record_history=False, max_pivots=cap, chunk=chunk)
+    last = out[-2] if sm.status == "error" else out[-1]
+    return sm, (sm.pivot_log, sm.status, str(out[-1]) if sm.status == "error" else None,
+                table_hash(last.table))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_every_fixture_block_vs_chain_vs_reference(block_mode, P):
+    """Every trajectory fixture: block chain == one-pivot chain == the reference's pivots, with
+    chunks that end inside and at block boundaries and terminal outcomes inside blocks."""
+    n_blk = 0
+    for label, cons, func, rec in CASES:
+        if len(func) not in (len(cons[0]) - 1, len(cons[0])) or len(func) < 2:
+            continue   # the reference raises IndexError there (f() needs x1, x2)
+        cap = trajectory_cap(rec)
+        block_mode(P)
+        sm, a = _solve(cons, func, cap, 7)
+        n_blk += sm._dev.block_plan() is not None
+        block_mode(1)
+        _, b = _solve(cons, func, cap, 7)
+        assert a == b, label
+        exp = [(s["i"], s["j"]) for s in rec["steps"] if "i" in s and s["i"] is not None]
+        assert a[0] == exp[:len(a[0])], label
+        if rec["outcome"]["kind"] in ("optimum", "error"):
+            assert a[3] == rec["steps"][-1]["hash"], label
+    assert n_blk > 250
+
+
+@pytest.mark.parametrize("kind,n,m,k,chunk,P", [
+    ("uniform", 1023, 1023, 203, 64, 4),
+    ("uniform", 1023, 1023, 120, 120, 8),
+    ("uniform", 999, 3000, 150, 50, 3),        # wide, odd C
+    ("uniform", 3001, 998, 150, 50, 5),        # tall, odd C
+    ("mixed", 1023, 1023, 400, 100, 4),        # phase 1 first
+    ("mixed", 700, 900, 200, 61, 7),
+    ("degenerate", 511, 511, 300, 100, 4),     # zero ratios, -0.0 classes
+    ("degenerate_mixed", 600, 300, 300, 100, 6),
+    ("uniform", 65535, 255, 40, 20, 4),        # very tall
+    ("mixed", 255, 65535, 40, 20, 4),          # very wide, phase 1
+])
+def test_block_vs_oracle(block_mode, kind, n, m, k, chunk, P):
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    import simplex
+    block_mode(P)
+    T = lp.dense_tableau(kind, 11, n, m)
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    assert sm._dev.block_plan()[1] == P
+    sm.solve(record_history=False, max_pivots=k, chunk=chunk)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    assert sm.pivots == done
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    got = sm._dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
+@pytest.mark.parametrize("P", [1, 2, 5, 8])
+def test_graph_and_eager_block_chains_agree(block_mode, P):
+    from simplex_mi355x import lp
+    import simplex
+    block_mode(P if P > 1 else 2)
+    T = lp.dense_tableau("mixed", 3, 700, 900)
+    a = simplex.SimplexMethod(T[:700].tolist(), T[700, :900].tolist())
+    b = simplex.SimplexMethod(T[:700].tolist(), T[700, :900].tolist())
+    a._dev.block = P
+    b._dev.block = P
+    a.solve(record_history=False, max_pivots=96, chunk=32, graph=True)
+    b.solve(record_history=False, max_pivots=96, chunk=32, graph=False)
+    block_mode(1)
+    c = simplex.SimplexMethod(T[:700].tolist(), T[700, :900].tolist())
+    c.solve(record_history=False, max_pivots=96, chunk=32)
+    assert a.pivot_log == b.pivot_log == c.pivot_log
+    ga, gb, gc = (x._dev.download().view(np.int64) for x in (a, b, c))
+    assert np.array_equal(ga, gb) and np.array_equal(ga, gc)
+
+
+def test_block_history_and_host_steps(block_mode):
+    """block chunk -> host pick_element/recalculate_matrix -> block chunk: control block state
+    carries over; the device x-history ring written by the planner equals the one-pivot chain's
+    and the lazy get_solution equals the eager one."""
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    import simplex
+    block_mode(4)
+    n, m = 300, 260
+    T = lp.dense_tableau("mixed", 9, n, m)
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    sm.solve(record_history=False, max_pivots=17, chunk=17)
+    for _ in range(3):
+        ok, i, j, _e = sm.pick_element()
+        assert ok
+        sm.recalculate_matrix()
+    sm.solve(record_history=False, max_pivots=22, chunk=11)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, 42, threads=8)
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    got = sm._dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    xa = sm._dev.read_xhist(0, 42)
+    block_mode(1)
+    ref = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    ref.solve(record_history=False, max_pivots=42, chunk=42)
+    assert np.array_equal(xa.view(np.int64), ref._dev.read_xhist(0, 42).view(np.int64))
+    recs = [r for r in load("random.json") if r["outcome"]["kind"] != "cap"]
+    for rec in recs[:6]:
+        cons, func = dec_input(rec["input"])
+        block_mode(3)
+        lazy = simplex.SimplexMethod([list(r) for r in cons], list(func)).get_solution(
+            lazy=True, chunk=5)
+        block_mode(1)
+        eager = simplex.SimplexMethod([list(r) for r in cons], list(func)).get_solution(
+            lazy=False)
+        assert len(lazy) == len(eager)
+        for a, b in zip(lazy, eager):
+            assert isinstance(a, simplex.Error) == isinstance(b, simplex.Error)
+            if isinstance(b, simplex.Error):
+                assert str(a) == str(b)
+                continue
+            assert (a.i, a.j, a.row, a.column) == (b.i, b.j, b.row, b.column)
+            assert np.array_equal(np.float64([a.x1, a.x2, a.optimum]).view(np.int64),
+                                  np.float64([b.x1, b.x2, b.optimum]).view(np.int64))
+            assert table_hash(a.table) == table_hash(b.table)
+
+
+def test_block_terminal_state_matches_chain(block_mode):
+    """A chain that stops inside a block leaves the same control block (status, selection,
+    first-negative slots, pivot count) and table as the one-pivot chain."""
+    import simplex
+    seen = 0
+    for rec in load("random.json"):
+        if rec["outcome"]["kind"] == "cap":
+            continue
+        cons, func = dec_input(rec["input"])
+        ctls = []
+        for P in (5, 1):
+            block_mode(P)
+            sm = simplex.SimplexMethod([list(r) for r in cons], list(func))
+            sm.solve(record_history=False, chunk=12)
+            c = sm._dev.read_ctl()
+            sp = int(c["npivots"]) & 1          # the slot of the table the chain stopped at
+            ctls.append((int(c["npivots"]), int(c["term"]), int(c["sel_status"]),
+                         int(c["sel_r"]), int(c["sel_c"]), int(c["negb"][sp]),
+                         int(c["negf"][sp]), table_hash(sm.table)))
+        assert ctls[0] == ctls[1], ctls
+        seen += 1
+    assert seen > 10
+
+
+@pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 6, 4), (16383, 16383, 5, 4)])
+def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
+    """BASELINE sizes through the default policy (4 pivots per sweep), a ragged last block."""
+    from simplex_mi355x import lp, _lib
+    from simplex_mi355x.device import DeviceTableau
+    from oracle import c_oracle
+    block_mode(0)
+    T = lp.dense_tableau("uniform", 0, n, m)
+    dev = DeviceTableau(T, n, m, m)
+    assert dev.block_plan()[1] == P
+    dev.run(k, graph=False)
+    ctl = dev.sync_state()
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=16)
+    assert int(ctl["npivots"]) == done == k
+    assert np.array_equal(dev.read_log(0, k), log)
+    got = dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
+def test_block_plan_policy(block_mode):
+    from simplex_mi355x import _lib
+    block_mode(0)
+    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 4
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4]) is None   # below 64 MiB
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 6)[1] == 6
+    assert _lib.block_plan([1024, 100, 1023, 1023, 1023, 0, 4], 4) is None  # sharded
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 9) is None
+    block_mode(1)
+    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64]) is None

@@ -1,0 +1,199 @@
+// multipivot_probe.hip -- how many Jordan steps can one HBM sweep of the tableau apply before the
+// fp64 arithmetic, not the stream, sets the time?  Applies P consecutive pivots per element
+// (pivot rows and per-row multipliers given, as a block sweep would have them from its planner)
+// with the reference's per-element expression (simplex.py:166-175: (x*e - pr*pc)/e per step),
+// either the compiler's IEEE division or the hoisted-reciprocal form of smx_resident.hpp, in
+// place or out of place, and prints us per sweep and the effective pivots/s.
+// Standalone: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off tools/multipivot_probe.hip \
+//             -o tools/multipivot_probe && tools/multipivot_probe [size]
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#pragma clang fp contract(off)
+
+#define CK(x)                                                                            \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess) {                                                          \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));    \
+            exit(1);                                                                     \
+        }                                                                                \
+    } while (0)
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+constexpr int kWave = 64, kBlock = 256, kWaves = kBlock / kWave, kChunk = 2 * kWave;
+constexpr int kMaxP = 8;
+
+struct Piv {
+    int r[kMaxP], c[kMaxP];
+    double e[kMaxP], y[kMaxP];
+};
+
+__device__ __forceinline__ bool fd_in(double x) {
+    const unsigned bexp = ((unsigned)(__double_as_longlong(x) >> 52)) & 0x7ffu;
+    return bexp - 896u <= 1152u - 896u;
+}
+
+template <bool FD>
+__device__ __forceinline__ double dv(double x, double e, double y) {
+    if (FD && fd_in(x) && fd_in(e)) {
+        const double q = x * y;
+        const double r = fma(-e, q, x);
+        return fma(r, y, q);
+    }
+    return x / e;
+}
+
+template <int P, bool FD>
+__global__ __launch_bounds__(kBlock) void k_multi(const double* __restrict__ Tin,
+                                                   double* Tout, int64_t ld, int R, int C,
+                                                   const double* __restrict__ PR,
+                                                   const double* __restrict__ M, Piv pv) {
+    const int lane = threadIdx.x & 63;
+    const int NW = gridDim.x * kWaves;
+    const int w = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunks = (C + kChunk - 1) / kChunk;
+    const int64_t units = (int64_t)nchunks * R;
+    const int qs = NW / nchunks, rs = NW % nchunks;
+    int i = w / nchunks, ch = w % nchunks;
+    int ch_pr = -1;
+    dbl2 pr[P];
+    constexpr int U = 2;
+    for (int64_t u = w; u < units; u += (int64_t)U * NW) {
+        int ii[U], cc[U];
+        dbl2 x[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            ii[k] = i;
+            cc[k] = ch;
+            ch += rs;
+            i += qs;
+            if (ch >= nchunks) {
+                ch -= nchunks;
+                ++i;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int j = cc[k] * kChunk + 2 * lane;
+            x[k] = dbl2{0.0, 0.0};
+            if (ii[k] < R && j < C)
+                x[k] = __builtin_nontemporal_load(
+                    reinterpret_cast<const dbl2*>(Tin + (int64_t)ii[k] * ld + j));
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int row = ii[k];
+            if (row >= R) continue;
+            const int j = cc[k] * kChunk + 2 * lane;
+            if (cc[k] != ch_pr) {
+                ch_pr = cc[k];
+#pragma unroll
+                for (int l = 0; l < P; ++l)
+                    pr[l] = (j < C) ? *reinterpret_cast<const dbl2*>(PR + (int64_t)l * ld + j)
+                                    : dbl2{0.0, 0.0};
+            }
+            double pc[P];
+#pragma unroll
+            for (int l = 0; l < P; ++l) pc[l] = M[(int64_t)row * kMaxP + l];
+            dbl2 v = x[k];
+#pragma unroll
+            for (int l = 0; l < P; ++l) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int jj = j + h;
+                    double num;
+                    if (row == pv.r[l])
+                        num = (jj == pv.c[l]) ? 1.0 : -v[h];
+                    else
+                        num = (jj == pv.c[l]) ? v[h] : (v[h] * pv.e[l] - pr[l][h] * pc[l]);
+                    v[h] = dv<FD>(num, pv.e[l], pv.y[l]);
+                }
+            }
+            if (j < C)
+                __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(Tout + (int64_t)row * ld + j));
+        }
+    }
+}
+
+template <int P, bool FD>
+float run(const double* a, double* b, int64_t ld, int R, int C, const double* PR, const double* M,
+          const Piv& pv, int grid, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    hipLaunchKernelGGL((k_multi<P, FD>), dim3(grid), dim3(kBlock), 0, 0, a, b, ld, R, C, PR, M, pv);
+    CK(hipEventRecord(e0));
+    for (int t = 0; t < reps; ++t)
+        hipLaunchKernelGGL((k_multi<P, FD>), dim3(grid), dim3(kBlock), 0, 0, a, b, ld, R, C, PR, M,
+                           pv);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / reps;
+}
+
+__global__ void k_fill(double* a, int64_t n, unsigned long long seed) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        unsigned long long z = (i + seed) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 31)) * 0xBF58476D1CE4E5B9ull;
+        a[i] = ((double)(z >> 11) / 9007199254740992.0) * 2.0 - 1.0;
+    }
+}
+
+template <int P>
+void row(const char* label, const double* a, double* b, int64_t ld, int R, int C, const double* PR,
+         const double* M, const Piv& pv, int grid, int reps) {
+    const double bytes = 16.0 * R * C;
+    const float t0 = run<P, false>(a, b, ld, R, C, PR, M, pv, grid, reps);
+    const float t1 = run<P, true>(a, b, ld, R, C, PR, M, pv, grid, reps);
+    printf("{\"size\": %d, \"P\": %d, \"mode\": \"%s\", \"ieee_us\": %.1f, \"fastdiv_us\": %.1f, "
+           "\"ieee_gbs\": %.0f, \"fastdiv_gbs\": %.0f, \"ieee_pivots_s\": %.0f, "
+           "\"fastdiv_pivots_s\": %.0f}\n",
+           R, P, label, t0 * 1e3, t1 * 1e3, bytes / t0 / 1e6, bytes / t1 / 1e6, P * 1e3 / t0,
+           P * 1e3 / t1);
+    fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? atoi(argv[1]) : 16384;
+    const int R = N, C = N;
+    const int64_t ld = C;
+    double *a, *b, *PR, *M;
+    CK(hipMalloc(&a, (size_t)R * ld * 8));
+    CK(hipMalloc(&b, (size_t)R * ld * 8));
+    CK(hipMalloc(&PR, (size_t)kMaxP * ld * 8));
+    CK(hipMalloc(&M, (size_t)R * kMaxP * 8));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, a, (int64_t)R * ld, 1ull);
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, PR, (int64_t)kMaxP * ld, 2ull);
+    hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, M, (int64_t)R * kMaxP, 3ull);
+    CK(hipDeviceSynchronize());
+    Piv pv;
+    for (int l = 0; l < kMaxP; ++l) {
+        pv.r[l] = (l * 977 + 5) % R;
+        pv.c[l] = (l * 1231 + 7) % C;
+        pv.e[l] = 0.75 + 0.125 * l;
+        pv.y[l] = 1.0 / pv.e[l];
+    }
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int reps = N >= 16384 ? 10 : 40;
+    for (int bpc : {4, 5, 8}) {
+        const int grid = cus * bpc;
+        char lab[64];
+        snprintf(lab, sizeof lab, "out-of-place bpc%d", bpc);
+        row<1>(lab, a, b, ld, R, C, PR, M, pv, grid, reps);
+        row<2>(lab, a, b, ld, R, C, PR, M, pv, grid, reps);
+        row<3>(lab, a, b, ld, R, C, PR, M, pv, grid, reps);
+        row<4>(lab, a, b, ld, R, C, PR, M, pv, grid, reps);
+        row<6>(lab, a, b, ld, R, C, PR, M, pv, grid, reps);
+        row<8>(lab, a, b, ld, R, C, PR, M, pv, grid, reps);
+    }
+    row<4>("in-place bpc5", a, a, ld, R, C, PR, M, pv, cus * 5, reps);
+    row<8>("in-place bpc5", a, a, ld, R, C, PR, M, pv, cus * 5, reps);
+    return 0;
+}
