@@ -386,10 +386,9 @@ int block_pivots(const smx_shape& s) {
 
 using BlkSweepFn = void (*)(double*, double*, int64_t, int, int, const BlkHdr*, const double*,
                            const double*);
-using BlkColsFn = void (*)(const double*, int64_t, int, int, int, int, const smx_ctl*, char*,
-                           int64_t, int64_t, int64_t, double*, int64_t);
-using BlkDecFn = void (*)(const double*, int64_t, int, int, int, int, int, int, smx_ctl*, char*,
-                          int64_t, int64_t, int64_t, int64_t, int32_t*, double*, int64_t);
+using BlkStepFn = void (*)(const double*, int64_t, int, int, int, int, int, int, int, smx_ctl*,
+                           BlkHdr*, smx_part*, double*, double*, double*, int32_t*, double*,
+                           int64_t);
 
 template <bool NTL>
 BlkSweepFn blk_sweep_fn_ntl(int P) {
@@ -405,30 +404,16 @@ BlkSweepFn blk_sweep_fn_ntl(int P) {
     }
 }
 
-BlkColsFn blk_cols_fn(int L) {
+BlkStepFn blk_step_fn(int L) {
     switch (L) {
-        case 0: return k_blk_cols<0>;
-        case 1: return k_blk_cols<1>;
-        case 2: return k_blk_cols<2>;
-        case 3: return k_blk_cols<3>;
-        case 4: return k_blk_cols<4>;
-        case 5: return k_blk_cols<5>;
-        case 6: return k_blk_cols<6>;
-        case 7: return k_blk_cols<7>;
-        default: return k_blk_cols<8>;
-    }
-}
-
-BlkDecFn blk_dec_fn(int L) {
-    switch (L) {
-        case 0: return k_blk_dec<0>;
-        case 1: return k_blk_dec<1>;
-        case 2: return k_blk_dec<2>;
-        case 3: return k_blk_dec<3>;
-        case 4: return k_blk_dec<4>;
-        case 5: return k_blk_dec<5>;
-        case 6: return k_blk_dec<6>;
-        default: return k_blk_dec<7>;
+        case 1: return k_blk_step<1>;
+        case 2: return k_blk_step<2>;
+        case 3: return k_blk_step<3>;
+        case 4: return k_blk_step<4>;
+        case 5: return k_blk_step<5>;
+        case 6: return k_blk_step<6>;
+        case 7: return k_blk_step<7>;
+        default: return k_blk_step<8>;
     }
 }
 
@@ -444,44 +429,44 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     return (int)hipGetLastError();
 }
 
-// k pivots in blocks of P: prime, then per block P x (decide, columns) and one sweep; publish.
-// ev (optional): 2 events per block recorded around its sweep.
+// k pivots in blocks of P: prime + first records, then per block P step launches and one sweep;
+// publish.  ev (optional): 2 events per block recorded around its sweep.
 int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, int P,
                        smx_ctl* ctl, char* blk, int32_t* log, double* xhist, int64_t log_cap,
                        hipStream_t st, hipEvent_t* ev = nullptr) {
     const BlkLayout L = blk_layout(s.rows + 1, s.ld, s.nparts);
+    BlkHdr* h = reinterpret_cast<BlkHdr*>(blk);
+    smx_part* parts = reinterpret_cast<smx_part*>(blk + L.parts);
+    double* mul = reinterpret_cast<double*>(blk + L.mul);
+    double* pr = reinterpret_cast<double*>(blk + L.pr);
+    double* fr = reinterpret_cast<double*>(blk + L.fr);
     const int fscan = fscan_of(s);
     const double* t0 = parity ? buf1 : buf0;
-    hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(kBlkDec), 0, st, t0, s.ld, s.rows, s.m, fscan,
-                       (const smx_ctl*)ctl, blk, L.fr);
-    hipLaunchKernelGGL(blk_cols_fn(0), dim3(s.nparts), dim3(kUpdBlock), 0, st, t0, s.ld, s.rows,
-                       s.m, P, parity, (const smx_ctl*)ctl, blk, L.parts, L.mul, L.pr, xhist,
-                       log_cap);
+    hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, t0, s.ld, s.rows, s.m, fscan,
+                       parity, (const smx_ctl*)ctl, h, fr);
+    hipLaunchKernelGGL(k_blk_first, dim3(s.nparts), dim3(kBlkNT), 0, st, t0, s.ld, s.rows, s.m,
+                       (const smx_ctl*)ctl, (const BlkHdr*)h, parts);
     int err = (int)hipGetLastError();
-    int p = parity, done = 0, b = 0;
+    int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
         const int Pb = (k - done < P) ? k - done : P;
         double* tin = p ? buf1 : buf0;
         double* toth = p ? buf0 : buf1;
-        for (int l = 0; l < Pb; ++l) {
-            hipLaunchKernelGGL(blk_dec_fn(l), dim3(1), dim3(kBlkDec), 0, st, (const double*)tin,
-                               s.ld, s.rows, s.m, s.flen, fscan, s.nparts, p, ctl, blk, L.parts,
-                               L.mul, L.pr, L.fr, log, xhist, log_cap);
-            hipLaunchKernelGGL(blk_cols_fn(l + 1), dim3(s.nparts), dim3(kUpdBlock), 0, st,
-                               (const double*)tin, s.ld, s.rows, s.m, Pb, p, (const smx_ctl*)ctl,
-                               blk, L.parts, L.mul, L.pr, xhist, log_cap);
-        }
+        for (int l = 1; l <= Pb; ++l)
+            hipLaunchKernelGGL(blk_step_fn(l), dim3(s.nparts), dim3(kBlkNT), 0, st,
+                               (const double*)tin, s.ld, s.rows, s.m, s.flen, fscan, Pb, p, bn,
+                               ctl, h, parts, mul, pr, fr, log, xhist, log_cap);
         err = (int)hipGetLastError();
-        if (ev) (void)hipEventRecord(ev[2 * b], st);
+        if (ev) (void)hipEventRecord(ev[2 * bn], st);
         if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, L, st);
-        if (ev) (void)hipEventRecord(ev[2 * b + 1], st);
+        if (ev) (void)hipEventRecord(ev[2 * bn + 1], st);
         p = (p + Pb) & 1;
         done += Pb;
-        ++b;
+        ++bn;
     }
     if (err) return err;
-    hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const char*)blk, L.parts,
-                       s.nparts, p, ctl);
+    hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)h,
+                       (const smx_part*)parts, s.nparts, blk_slot(0, 1, bn), p, ctl);
     return (int)hipGetLastError();
 }
 
