@@ -10,60 +10,75 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 // Why: one pivot reads and writes every element once (16 B), so a chain of single-pivot sweeps is
 // pinned at the copy rate of HBM (16384^2: ~815 us per pivot, 95 % of the measured copy ceiling).
-// But the per-element arithmetic is only two multiplies, a subtract and a division:
-// tools/multipivot_probe.hip measured 3 chained updates per element in the time of 1, 4 at +7 %.
+// The per-element arithmetic is only two multiplies, a subtract and a division, and
+// tools/compute_probe.hip measured ~5 T element-steps/s of it on the chip against ~0.33 T
+// elements/s that HBM streams: one sweep can carry several pivots.
 //
 // Every value of T_{k+l} follows from T_k, the pivot rows and the per-row multipliers of the
 // steps before it, by the update's own expression (the look-ahead's nv(), applied l times):
-//     chain(x = T_k[i][j], L):  for q < L:
+//     chain(x = T_k[i][j], l):  for q < l:
 //         num = (i == r_q) ? (j == c_q ? 1.0 : -x) : (j == c_q ? x : x*e_q - pr_q[j]*mul[i][q])
 //         x = num / e_q
 //     pr_q      = row r_q of T_{k+q}        (the pivot row of step k+q, C doubles)
 //     mul[i][q] = T_{k+q}[i][c_q]           (row i's pivot-column entry before step k+q)
 // so chain(T_k[i][j], l) IS T_{k+l}[i][j], bit for bit (same operations on the same operands in
-// the same order as l single-pivot sweeps).  A block of P pivots on T_k is then:
-//   k_blk_dec(l), l = 0..P-1   one workgroup: decision l from the records of step k+l (phase 1:
-//                              first positive entry of the first-negative-b row, simplex.py:72-91;
-//                              phase 2: ratio arg-min, :93-141), pr_l, the f-row of T_{k+l+1}
-//                              (kept in `fr`) and its first negative entry (the next entering
-//                              column), and the pivot's log / label / x-history bookkeeping;
-//   k_blk_cols(l + 1)          nparts workgroups: mul[i][l] for every row, then the records of
-//                              step k+l+1 (first negative "-b" row, ratio candidates on the new
-//                              entering column) from chains of length l+1;
-//   k_blk_sweep                every element T_k -> T_{k+peff} through the peff decided steps,
-//                              out of place when peff is odd and in place when it is even, so the
-//                              table after d pivots is in buf[(parity + d) & 1] exactly as in the
-//                              single-pivot chains.  In place is safe: each element is read and
-//                              written by the same lane and nothing reads T_k after the planner.
-// k_blk_cols(P) computes the records of the NEXT block's first step (chains of length P from this
-// block's T_k), so a block is 2P + 1 launches.  A terminal outcome at step l latches ctl->term;
-// the sweep still applies the l pivots decided before it and every later kernel does nothing.
+// the same order as l single-pivot sweeps).  A chain of blocks on T_k:
+//   k_blk_prime + k_blk_first   once per chain: the f-row of T_k (`fr`), its first negative entry
+//                               and the records of step k (first negative "-b" row and ratio
+//                               candidates on that column, the layout of la_partial);
+//   k_blk_step<L>, L = 1..P     one launch per pivot (nparts workgroups): every workgroup decides
+//                               block step D = L-1 from its records (phase 1: first positive of
+//                               the first-negative-b row, simplex.py:72-91; phase 2: ratio arg-min,
+//                               :93-141) and derives the pivot row values it needs on the fly;
+//                               workgroup b stores slice b of pr_D and of the next f-row; each
+//                               scans the new f-row for its first negative entry (early exit);
+//                               then mul[i][D] for its rows and the records of step L (chains of
+//                               length L); workgroup 0 does the pivot's log / label / history
+//                               bookkeeping;
+//   k_blk_sweep                 every element T_k -> T_{k+peff} through the peff decided steps,
+//                               out of place when peff is odd and in place when it is even, so the
+//                               table after d pivots is in buf[(parity + d) & 1] exactly as in the
+//                               single-pivot chains.  In place is safe: each element is read and
+//                               written by the same lane and nothing reads T_k after the planner.
+// k_blk_step<P> builds the records of the NEXT block's first step (chains of length P from this
+// block's T_k), so a block is P + 1 launches.  A terminal outcome at step D latches ctl->term;
+// the sweep still applies the D pivots decided before it and every later kernel does nothing.
 constexpr int kBlkMax = 8;           // pivots per block (mul row stride)
-constexpr int kBlkDec = 1024;        // k_blk_dec / k_blk_prime workgroup
+constexpr int kBlkSlots = kBlkMax + 2;   // record / cf slots: steps 1..P-1, and two for step 0
+constexpr int kBlkNT = kUpdBlock;    // planner workgroup
+constexpr int kBlkScan = 4 * kBlkNT; // columns per early-exit scan round
 
 struct BlkHdr {
     int32_t peff;                    // pivots of this block decided so far (the sweep's count)
-    int32_t cf;                      // first j < fscan with fr[j] < 0 (SMX_NONE: none)
-    int32_t pad[2];
+    int32_t pad0;
+    int32_t cfs[kBlkSlots];          // first j < fscan with f[j] < 0 of the step in that slot
     int32_t r[kBlkMax], c[kBlkMax];
     int32_t ok[kBlkMax];             // e inside the fast-division window (fd_prep)
+    int32_t pad1;
     double e[kBlkMax], y[kBlkMax];   // pivot element and its refined reciprocal (fd_prep)
 };
-static_assert(sizeof(BlkHdr) <= 256, "block header");
+static_assert(sizeof(BlkHdr) <= 512, "block header");
 
-// Scratch layout (byte offsets; smx_block_bytes): header | records [kBlkMax][nparts] |
-// mul [R][kBlkMax] | pr [kBlkMax][ld] | fr [ld]
+// record / cf slot of block step l: 1..P-1 their own; step 0 of block number bn (the next block's
+// first step, built by k_blk_step<P>) alternates between two slots, so no launch reads the slot
+// it writes even at P = 1
+__host__ __device__ __forceinline__ int blk_slot(int l, int P, int bn) {
+    return l == 0 ? kBlkMax + (bn & 1) : (l == P ? kBlkMax + ((bn + 1) & 1) : l);
+}
+
+// Scratch layout (byte offsets; smx_block_bytes): header | records [kBlkSlots][nparts] |
+// mul [R][kBlkMax] | pr [kBlkMax][ld] | fr [2][ld] (the f-row by step parity)
 struct BlkLayout {
     int64_t parts, mul, pr, fr, bytes;
 };
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     BlkLayout L;
-    L.parts = 256;
-    L.mul = blk_align(L.parts + (int64_t)kBlkMax * nparts * 32);
+    L.parts = 512;
+    L.mul = blk_align(L.parts + (int64_t)kBlkSlots * nparts * 32);
     L.pr = blk_align(L.mul + R * kBlkMax * 8);
     L.fr = blk_align(L.pr + (int64_t)kBlkMax * ld * 8);
-    L.bytes = blk_align(L.fr + ld * 8);
+    L.bytes = blk_align(L.fr + 2 * ld * 8);
     return L;
 }
 
@@ -100,119 +115,78 @@ __device__ __forceinline__ void blk_load_col(const double* __restrict__ pr, int6
     for (int q = 0; q < L; ++q) p[q] = pr[(int64_t)q * ld + j];
 }
 
-__device__ __forceinline__ void blk_load_piv(const BlkHdr* h, int L, BlkPiv* s_pv) {
-    const int t = threadIdx.x;
-    if (t < L) {
-        s_pv->r[t] = h->r[t];
-        s_pv->c[t] = h->c[t];
-        s_pv->e[t] = h->e[t];
-    }
+// Row r of T_{k+D} at column j (the pivot row of block step D; mqr = mul[r][0..D))
+template <int D>
+__device__ __forceinline__ double blk_prv(const double* __restrict__ T, int64_t ld, int r, int j,
+                                          const BlkPiv& pv, const double* __restrict__ pr,
+                                          const double* mqr) {
+    double p[kBlkMax];
+    blk_load_col<D>(pr, ld, j, p);
+    return blk_chain<D>(T[(int64_t)r * ld + j], r, j, pv, p, mqr);
 }
 
-// Chain start: the f-row of T into `fr` and its first negative entry (simplex.py:94-98).
-__global__ __launch_bounds__(kBlkDec) void k_blk_prime(const double* __restrict__ T, int64_t ld,
-                                                        int rows, int m, int fscan,
-                                                        const smx_ctl* __restrict__ ctl,
-                                                        char* __restrict__ blk, int64_t off_fr) {
-    __shared__ int s_tmp[kBlkDec / kWave];
+// The f-row entry after a pivot (row `rows` is never the pivot row): simplex.py:159-160/:166-175
+__device__ __forceinline__ double blk_fnew(double x, double pj, int j, int c, double e,
+                                           double fc) {
+    const double a = x * e;
+    const double b = pj * fc;
+    return ((j == c) ? x : (a - b)) / e;
+}
+
+// Chain start: the f-row of T into fr[parity] and its first negative entry (simplex.py:94-98).
+__global__ __launch_bounds__(1024) void k_blk_prime(const double* __restrict__ T, int64_t ld,
+                                                     int rows, int m, int fscan, int parity,
+                                                     const smx_ctl* __restrict__ ctl,
+                                                     BlkHdr* __restrict__ h,
+                                                     double* __restrict__ fr) {
+    __shared__ int s_tmp[1024 / kWave];
     if (ctl->term) return;
     const int C = m + 1;
     const double* f = T + (int64_t)rows * ld;
-    double* fr = reinterpret_cast<double*>(blk + off_fr);
+    double* fo = fr + (int64_t)parity * ld;
     int nf = SMX_NONE;
-    for (int j = threadIdx.x; j < C; j += kBlkDec) {
+    for (int j = threadIdx.x; j < C; j += 1024) {
         const double v = f[j];
-        fr[j] = v;
+        fo[j] = v;
         if (j < fscan && v < 0.0 && j < nf) nf = j;
     }
-    nf = block_min_int<kBlkDec>(nf, s_tmp);
+    nf = block_min_int<1024>(nf, s_tmp);
     if (threadIdx.x == 0) {
-        BlkHdr* h = reinterpret_cast<BlkHdr*>(blk);
-        h->cf = nf;
+        h->cfs[blk_slot(0, 1, 0)] = nf;
         h->peff = 0;
     }
 }
 
-// The records of step k+L (chains of length L from T_k) and, for L >= 1, mul[i][L-1] and the
-// x-history entry of step k+L-1 (the new "-b" entry of the rows labelled x1 / x2).  Workgroup b
-// of nparts covers rows b*NT + tid + q*nparts*NT (the layout of la_partial); L == P is the next
-// block's first step (record slot 0).
-template <int L>
-__global__ __launch_bounds__(kUpdBlock) void k_blk_cols(
-    const double* __restrict__ T, int64_t ld, int rows, int m, int P, int parity,
-    const smx_ctl* __restrict__ ctl, char* __restrict__ blk, int64_t off_parts, int64_t off_mul,
-    int64_t off_pr, double* __restrict__ xhist, int64_t log_cap) {
-    constexpr int NT = kUpdBlock;
-    __shared__ BlkPiv s_pv;
-    __shared__ int s_cf;
-    __shared__ int s_b[NT / kWave];
-    __shared__ First s_f[NT / kWave];
-    __shared__ Cand s_c[NT / kWave];
-    if (ctl->term) return;
-    const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk);
-    smx_part* parts = reinterpret_cast<smx_part*>(blk + off_parts);
-    double* mul = reinterpret_cast<double*>(blk + off_mul);
-    const double* pr = reinterpret_cast<const double*>(blk + off_pr);
+// Workgroup partial of the records (first negative "-b" row; first ratio candidate and best key)
+struct BlkRec {
+    int nb;
+    First f;
+    Cand bc;
+};
+
+__device__ __forceinline__ void blk_rec_add(BlkRec& R, int i, double bv, bool has_a, double a) {
+    if (bv < 0.0 && i < R.nb) R.nb = i;                     // simplex.py:73-76
+    if (has_a && a != 0.0) {                                // simplex.py:112 (NaN counts)
+        const double v = bv / a;                            // simplex.py:115
+        if (i < R.f.idx) {
+            R.f.idx = i;
+            R.f.v = v;
+        }
+        if (!isnan(v)) {
+            const Cand x = classify(v, i);
+            if (better(x, R.bc)) R.bc = x;
+        }
+    }
+}
+
+__device__ __forceinline__ void blk_rec_store(BlkRec R, smx_part* out) {
+    __shared__ int s_b[kBlkNT / kWave];
+    __shared__ First s_f[kBlkNT / kWave];
+    __shared__ Cand s_c[kBlkNT / kWave];
     const int tid = threadIdx.x;
-    blk_load_piv(h, L, &s_pv);
-    if (tid == 0) s_cf = h->cf;
-    __syncthreads();
-    const int cf = s_cf;
-    const int cp = L > 0 ? s_pv.c[L > 0 ? L - 1 : 0] : 0;
-    // x-history of step k+L-1: rows of labels x1 / x2 after it (k_blk_dec moved the labels)
-    int hx0 = -1, hx1 = -1;
-    int64_t hslot = 0;
-    if (L > 0 && xhist != nullptr && log_cap > 0) {
-        const int sp = (parity + L) & 1;
-        hx0 = ctl->xpos[sp][0];
-        hx1 = ctl->xpos[sp][1];
-        hslot = 2 * ((ctl->npiv[sp] - 1) % log_cap);
-    }
-    // the pivot rows at the three columns this kernel reads (uniform across the workgroup)
-    double pp[kBlkMax], pb[kBlkMax], pa[kBlkMax];
-    blk_load_col<(L > 1 ? L - 1 : 0)>(pr, ld, cp, pp);
-    blk_load_col<L>(pr, ld, m, pb);
-    if (cf != SMX_NONE) blk_load_col<L>(pr, ld, cf, pa);
-    const int b = blockIdx.x, nparts = gridDim.x;
-    int nb = SMX_NONE;
-    First f{SMX_NONE, 0.0};
-    Cand bc = cand_none();
-    for (int i = b * NT + tid; i < rows; i += nparts * NT) {
-        const double* row = T + (int64_t)i * ld;
-        double* mr = mul + (int64_t)i * kBlkMax;
-        // every load of the row first: three strided entries and the row's multipliers
-        const double xp = L > 0 ? row[cp] : 0.0;
-        const double xb = row[m];
-        const double xa = cf != SMX_NONE ? row[cf] : 0.0;
-        double mq[kBlkMax];
-#pragma unroll
-        for (int q = 0; q + 1 < L; ++q) mq[q] = mr[q];
-        if (L > 0) {
-            mq[L > 0 ? L - 1 : 0] = blk_chain<(L > 1 ? L - 1 : 0)>(xp, i, cp, s_pv, pp, mq);
-            mr[L > 0 ? L - 1 : 0] = mq[L > 0 ? L - 1 : 0];
-        }
-        const double bv = blk_chain<L>(xb, i, m, s_pv, pb, mq);
-        if (i == hx0) xhist[hslot] = bv;
-        if (i == hx1) xhist[hslot + 1] = bv;
-        if (bv < 0.0 && i < nb) nb = i;                      // simplex.py:73-76
-        if (cf != SMX_NONE) {
-            const double a = blk_chain<L>(xa, i, cf, s_pv, pa, mq);
-            if (a != 0.0) {                                 // simplex.py:112 (NaN counts)
-                const double v = bv / a;                    // simplex.py:115
-                if (i < f.idx) {
-                    f.idx = i;
-                    f.v = v;
-                }
-                if (!isnan(v)) {
-                    const Cand x = classify(v, i);
-                    if (better(x, bc)) bc = x;
-                }
-            }
-        }
-    }
-    nb = wave_min_int(nb);
-    f = wave_first(f);
-    bc = wave_best(bc);
+    int nb = wave_min_int(R.nb);
+    First f = wave_first(R.f);
+    Cand bc = wave_best(R.bc);
     const int wid = tid >> 6;
     if ((tid & 63) == 0) {
         s_b[wid] = nb;
@@ -221,7 +195,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_cols(
     }
     __syncthreads();
     if (tid == 0) {
-        for (int w = 1; w < NT / kWave; ++w) {
+        for (int w = 1; w < kBlkNT / kWave; ++w) {
             nb = min(nb, s_b[w]);
             if (s_f[w].idx < f.idx) f = s_f[w];
             if (better(s_c[w], bc)) bc = s_c[w];
@@ -233,43 +207,67 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_cols(
         pt.best_cls = bc.cls;
         pt.best_i = bc.idx;
         pt.best_v = bc.v;
-        const int slot = (L == P) ? 0 : L;
-        parts[(int64_t)slot * nparts + b] = pt;
+        *out = pt;
     }
 }
 
-// Decision L of the block (step k+L, parity slot sp = (parity + L) & 1) and everything the
-// sweep and the next planning step need from it.  One workgroup.
+// Records of a chain's first step, straight from T (workgroup b of nparts: rows b*NT + tid +
+// q*nparts*NT, the layout of la_partial).
+__global__ __launch_bounds__(kBlkNT) void k_blk_first(const double* __restrict__ T, int64_t ld,
+                                                      int rows, int m,
+                                                      const smx_ctl* __restrict__ ctl,
+                                                      const BlkHdr* __restrict__ h,
+                                                      smx_part* __restrict__ parts) {
+    if (ctl->term) return;
+    const int cf = h->cfs[blk_slot(0, 1, 0)];
+    const int b = blockIdx.x, nparts = gridDim.x;
+    BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
+    for (int i = b * kBlkNT + (int)threadIdx.x; i < rows; i += nparts * kBlkNT) {
+        const double* row = T + (int64_t)i * ld;
+        const double bv = row[m];
+        const double a = cf != SMX_NONE ? row[cf] : 0.0;
+        blk_rec_add(R, i, bv, cf != SMX_NONE, a);
+    }
+    blk_rec_store(R, parts + (int64_t)blk_slot(0, 1, 0) * nparts + b);
+}
+
+// One pivot of the block: decide block step D = L-1 and build the records of step L.
 template <int L>
-__global__ __launch_bounds__(kBlkDec) void k_blk_dec(
-    const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int nparts,
-    int parity, smx_ctl* __restrict__ ctl, char* __restrict__ blk, int64_t off_parts,
-    int64_t off_mul, int64_t off_pr, int64_t off_fr, int32_t* __restrict__ log,
-    double* __restrict__ xhist, int64_t log_cap) {
-    constexpr int NT = kBlkDec;
+__global__ __launch_bounds__(kBlkNT) void k_blk_step(
+    const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int P,
+    int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
+    smx_part* __restrict__ parts, double* __restrict__ mul, double* __restrict__ pr,
+    double* __restrict__ fr, int32_t* __restrict__ log, double* __restrict__ xhist,
+    int64_t log_cap) {
+    constexpr int D = L - 1;
+    constexpr int NT = kBlkNT;
     __shared__ BlkPiv s_pv;
     __shared__ int s_tmp[NT / kWave];
     __shared__ Decision s_d;
-    __shared__ int s_nb, s_cf;
-    BlkHdr* h = reinterpret_cast<BlkHdr*>(blk);
+    __shared__ int s_nb, s_c;
+    __shared__ double s_e, s_fc, s_pm, s_pa;
     const int tid = threadIdx.x;
+    const int b = blockIdx.x, G = gridDim.x;
     if (ctl->term) {
-        if (L == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain sweeps nothing
+        if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
         return;
     }
-    const smx_part* parts = reinterpret_cast<const smx_part*>(blk + off_parts) + (int64_t)L * nparts;
-    double* mul = reinterpret_cast<double*>(blk + off_mul);
-    double* pr = reinterpret_cast<double*>(blk + off_pr);
-    double* fr = reinterpret_cast<double*>(blk + off_fr);
-    const int sp = (parity + L) & 1;
-    blk_load_piv(h, L, &s_pv);
+    const int sp = (parity + D) & 1;   // step parity of block step D
+    const int C = m + 1;
+    if (tid < D) {
+        s_pv.r[tid] = h->r[tid];
+        s_pv.c[tid] = h->c[tid];
+        s_pv.e[tid] = h->e[tid];
+    }
+    // the decision of step D from its records (every workgroup, identically)
     if (tid < kWave) {
         smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
-        if (tid < nparts) rec = parts[tid];
-        const int c = h->cf;
-        int nb = wave_min_int(rec.p1col);
-        First f = wave_first(First{rec.first, rec.first_v});
-        Cand b = wave_best(Cand{rec.best_cls, rec.best_i, rec.best_v});
+        const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * G;
+        if (tid < G) rec = slot[tid];
+        const int c = h->cfs[blk_slot(D, P, bn)];
+        const int nb = wave_min_int(rec.p1col);
+        const First f = wave_first(First{rec.first, rec.first_v});
+        const Cand bb = wave_best(Cand{rec.best_cls, rec.best_i, rec.best_v});
         Decision d;
         d.c = c;
         d.r = SMX_NONE;
@@ -281,129 +279,218 @@ __global__ __launch_bounds__(kBlkDec) void k_blk_dec(
                 d.status = SMX_NOT_CONVERGE;                       // simplex.py:138-139
             } else if (isnan(f.v)) {
                 d.r = f.idx;                                       // simplex.py:117-121
-            } else if (b.cls >= 2) {
+            } else if (bb.cls >= 2) {
                 d.status = SMX_NOT_CONVERGE;
             } else {
-                d.r = b.idx;
+                d.r = bb.idx;
             }
+        } else {
+            d.r = nb;                  // phase 1: the column comes from the row scan below
+            d.c = SMX_NONE;
         }
         if (tid == 0) {
             s_nb = nb;
-            s_cf = c;
             s_d = d;
+            s_c = c;                   // cf of step D (the terminal state's negf)
         }
     }
     __syncthreads();
     const int nb = s_nb;
     Decision d = s_d;
-    const int C = m + 1;
-    double* prl = pr + (int64_t)L * ld;
-    if (nb != SMX_NONE || d.status == SMX_PIVOT) {
-        // the pivot row of T_{k+L} (phase 1: also its first positive entry, simplex.py:81-85)
-        const int r = nb != SMX_NONE ? nb : d.r;
-        const double* row = T + (int64_t)r * ld;
-        const double* mrow = mul + (int64_t)r * kBlkMax;
-        double mq[kBlkMax];
-#pragma unroll
-        for (int q = 0; q < L; ++q) mq[q] = mrow[q];
-        int p1 = SMX_NONE;
-#pragma unroll 2
-        for (int j = tid; j < C; j += NT) {
-            double p[kBlkMax];
-            blk_load_col<L>(pr, ld, j, p);
-            const double v = blk_chain<L>(row[j], r, j, s_pv, p, mq);
-            prl[j] = v;
-            if (j < m && v > 0.0 && j < p1) p1 = j;
-        }
-        if (nb != SMX_NONE) {
-            p1 = block_min_int<NT>(p1, s_tmp);
-            d.r = nb;
-            d.c = p1;
-            d.status = (p1 == SMX_NONE) ? SMX_INCORRECT : SMX_PIVOT;
-        }
-    }
-    if (d.status != SMX_PIVOT) {
-        if (tid == 0) {
-            ctl->sel_status = d.status;
-            ctl->sel_r = d.r;
-            ctl->sel_c = d.c;
-            ctl->negb[sp] = nb;         // the state of T_{k+L}, where the chain stops
-            ctl->negf[sp] = s_cf;
+    auto terminal = [&](const Decision& dd) {
+        if (b == 0 && tid == 0) {
+            ctl->sel_status = dd.status;
+            ctl->sel_r = dd.r;
+            ctl->sel_c = dd.c;
+            ctl->negb[sp] = nb;        // the state of T_{k+D}, where the chain stops
+            ctl->negf[sp] = s_c;
             ctl->term = 1;
-            h->peff = L;
+            h->peff = D;
         }
+    };
+    if (d.status != SMX_PIVOT) {
+        terminal(d);
         return;
     }
-    __syncthreads();                    // prl complete
-    const int r = d.r, c = d.c;
-    const double e = prl[c];
-    const double fc = fr[c];
-    __syncthreads();                    // every thread has fc before fr[c] changes
-    if (tid == 0) {
-        // bookkeeping of the pivot (its latency overlaps the f-row pass of the other waves);
-        // the x-history value of a basic label is written by k_blk_cols<L + 1>
-        const FastDiv fd = fd_prep(e);
-        mul[(int64_t)rows * kBlkMax + L] = fc;
-        h->r[L] = r;
-        h->c[L] = c;
-        h->e[L] = e;
-        h->y[L] = fd.y;
-        h->ok[L] = fd.ok ? 1 : 0;
-        const int64_t k = ctl->npiv[sp];
-        if (log_cap > 0) {
-            log[2 * (k % log_cap)] = r;
-            log[2 * (k % log_cap) + 1] = c;
+    const int r = d.r;
+    double mqr[kBlkMax];
+#pragma unroll
+    for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)r * kBlkMax + q];
+    const double* fo = fr + (int64_t)sp * ld;          // f-row of T_{k+D}
+    double* fn = fr + (int64_t)(sp ^ 1) * ld;          // f-row of T_{k+L}
+    double* prD = pr + (int64_t)D * ld;
+    if (nb != SMX_NONE) {
+        // phase 1: first j < m with T_{k+D}[r][j] > 0 (simplex.py:81-85), early exit by rounds
+        int p1 = SMX_NONE;
+        for (int j0 = 0; j0 < m && p1 == SMX_NONE; j0 += kBlkScan) {
+            int mine = SMX_NONE;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = j0 + k * NT + tid;
+                if (j < m && blk_prv<D>(T, ld, r, j, s_pv, pr, mqr) > 0.0 && j < mine) mine = j;
+            }
+            p1 = block_min_int<NT>(mine, s_tmp);
         }
-        ctl->npivots = k + 1;
-        ctl->npiv[sp ^ 1] = k + 1;
+        if (p1 == SMX_NONE) {
+            d.c = SMX_NONE;
+            d.status = SMX_INCORRECT;   // simplex.py:88-89
+            terminal(d);
+            return;
+        }
+        d.c = p1;
+    }
+    const int c = d.c;
+    if (tid == 0) {
+        s_e = blk_prv<D>(T, ld, r, c, s_pv, pr, mqr);
+        s_fc = fo[c];
+        s_pm = blk_prv<D>(T, ld, r, m, s_pv, pr, mqr);
+    }
+    __syncthreads();
+    const double e = s_e, fc = s_fc;
+    // slice b of the pivot row and of the next f-row
+    {
+        const int S = ((C + G - 1) / G + 1) & ~1;
+        const int s1 = min(C, (b + 1) * S);
+        for (int j = b * S + tid; j < s1; j += NT) {
+            const double v = blk_prv<D>(T, ld, r, j, s_pv, pr, mqr);
+            prD[j] = v;
+            fn[j] = blk_fnew(fo[j], v, j, c, e, fc);
+        }
+    }
+    // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
+    int cf = SMX_NONE;
+    for (int j0 = 0; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
+        int mine = SMX_NONE;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = j0 + k * NT + tid;
+            if (j < fscan) {
+                const double v = blk_prv<D>(T, ld, r, j, s_pv, pr, mqr);
+                if (blk_fnew(fo[j], v, j, c, e, fc) < 0.0 && j < mine) mine = j;
+            }
+        }
+        cf = block_min_int<NT>(mine, s_tmp);
+    }
+    if (tid == 0) s_pa = cf != SMX_NONE ? blk_prv<D>(T, ld, r, cf, s_pv, pr, mqr) : 0.0;
+    // the labels after this pivot (simplex.py:152), identically in every workgroup
+    const int hx0 = move_label(ctl->xpos[sp][0], r, c);
+    const int hx1 = move_label(ctl->xpos[sp][1], r, c);
+    const int64_t kpiv = ctl->npiv[sp];
+    if (b == 0 && tid == 0) {
+        const FastDiv fd = fd_prep(e);
+        mul[(int64_t)rows * kBlkMax + D] = fc;
+        h->r[D] = r;
+        h->c[D] = c;
+        h->e[D] = e;
+        h->y[D] = fd.y;
+        h->ok[D] = fd.ok ? 1 : 0;
+        h->peff = D + 1;
+        h->cfs[blk_slot(L, P, bn)] = cf;
+        if (log_cap > 0) {
+            log[2 * (kpiv % log_cap)] = r;
+            log[2 * (kpiv % log_cap) + 1] = c;
+        }
+        ctl->npivots = kpiv + 1;
+        ctl->npiv[sp ^ 1] = kpiv + 1;
         ctl->sel_status = SMX_PIVOT;
         ctl->sel_r = r;
         ctl->sel_c = c;
         ctl->sel_e = e;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int code = move_label(ctl->xpos[sp][q], r, c);
-            ctl->xpos[sp ^ 1][q] = code;
-            if (xhist && log_cap > 0 && code < 0) xhist[2 * (k % log_cap) + q] = 0.0;  // :60-66
+        ctl->xpos[sp ^ 1][0] = hx0;
+        ctl->xpos[sp ^ 1][1] = hx1;
+        if (xhist && log_cap > 0) {                  // non-basic labels: 0 (simplex.py:60-66)
+            if (hx0 < 0) xhist[2 * (kpiv % log_cap)] = 0.0;
+            if (hx1 < 0) xhist[2 * (kpiv % log_cap) + 1] = 0.0;
         }
     }
-    // the f-row of T_{k+L+1} (row `rows`, never the pivot row) and its first negative entry
-    int nf = SMX_NONE;
-#pragma unroll 2
-    for (int j = tid; j < C; j += NT) {
-        const double x = fr[j];
-        const double a = x * e;
-        const double b = prl[j] * fc;
-        const double v = ((j == c) ? x : (a - b)) / e;
-        fr[j] = v;
-        if (j < fscan && v < 0.0 && j < nf) nf = j;
-    }
-    nf = block_min_int<NT>(nf, s_tmp);
+    __syncthreads();
+    // step L's pivots in LDS-broadcast form: s_pv[D] = this pivot
     if (tid == 0) {
-        h->peff = L + 1;
-        h->cf = nf;
+        s_pv.r[D] = r;
+        s_pv.c[D] = c;
+        s_pv.e[D] = e;
     }
+    __syncthreads();
+    // the pivot rows at the columns the row pass reads (uniform)
+    double pc_[kBlkMax], pm_[kBlkMax], pa_[kBlkMax];
+    blk_load_col<D>(pr, ld, c, pc_);
+    blk_load_col<D>(pr, ld, m, pm_);
+    pm_[D] = s_pm;
+    if (cf != SMX_NONE) {
+        blk_load_col<D>(pr, ld, cf, pa_);
+        pa_[D] = s_pa;
+    }
+    const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
+    BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
+    for (int i = b * NT + tid; i < rows; i += G * NT) {
+        const double* row = T + (int64_t)i * ld;
+        double* mr = mul + (int64_t)i * kBlkMax;
+        const double xc = row[c];
+        const double xb = row[m];
+        const double xa = cf != SMX_NONE ? row[cf] : 0.0;
+        double mq[kBlkMax];
+#pragma unroll
+        for (int q = 0; q < D; ++q) mq[q] = mr[q];
+        mq[D] = blk_chain<D>(xc, i, c, s_pv, pc_, mq);   // T_{k+D}[i][c]
+        mr[D] = mq[D];
+        const double bv = blk_chain<L>(xb, i, m, s_pv, pm_, mq);
+        if (xhist && log_cap > 0) {
+            if (i == hx0) xhist[hslot] = bv;
+            if (i == hx1) xhist[hslot + 1] = bv;
+        }
+        const double a = cf != SMX_NONE ? blk_chain<L>(xa, i, cf, s_pv, pa_, mq) : 0.0;
+        blk_rec_add(R, i, bv, cf != SMX_NONE, a);
+    }
+    blk_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);
 }
 
-// The sweep: T_k -> T_{k+P} for every element (P = peff pivots of this block).  The pivot data
-// is wave-uniform (scalar loads); the division takes fd_div's hoisted form when the whole wave's
-// numerators lie in its window (one vote per unit and pivot), else the hardware division for
-// the lanes outside it -- bit-identical either way (smx_resident.hpp).
+// The sweep: T_k -> T_{k+P} for every element (P = peff pivots of this block).
+// Exact per element with either division (fd_div's window form is bit-identical inside its
+// window; smx_resident.hpp).  Fast path for a unit whose row is not a pivot row and whose chunk
+// holds no pivot column: numerators in the window form, with the smallest and largest |num| of
+// the whole chain tracked per lane; ONE wave vote per unit checks them against the window (and
+// the result against NaN) and otherwise the unit is recomputed with the hardware division.
+constexpr double kFdMinAbs = 0x1p-127;   // biased exponent 896
+constexpr double kFdMaxAbs = 0x1p130;    // biased exponent 1152 is the last inside
+
+template <int P>
+__device__ __forceinline__ dbl2 blk_exact(dbl2 v, int row, int j, const int* rq, const int* cq,
+                                          const double* eq, const dbl2* prs, const double* pc) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int jj = j + hh;
+            double num;
+            if (row == rq[q]) {
+                num = (jj == cq[q]) ? 1.0 : -v[hh];
+            } else {
+                const double a = v[hh] * eq[q];
+                const double b = prs[q][hh] * pc[q];
+                num = (jj == cq[q]) ? v[hh] : (a - b);
+            }
+            v[hh] = num / eq[q];
+        }
+    }
+    return v;
+}
+
 template <int P, bool NTL>
 __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, int64_t ld, int R,
                                                int C, const BlkHdr* __restrict__ h,
                                                const double* __restrict__ pr,
                                                const double* __restrict__ mul) {
     const int lane = threadIdx.x & (kWave - 1);
-    int rq[P], cq[P], okq[P];
+    int rq[P], cq[P];
     double eq[P], yq[P];
+    bool allok = true;
 #pragma unroll
     for (int q = 0; q < P; ++q) {
         rq[q] = h->r[q];
         cq[q] = h->c[q];
-        okq[q] = h->ok[q];
         eq[q] = h->e[q];
         yq[q] = h->y[q];
+        allok = allok && h->ok[q] != 0;
     }
     constexpr int kChunk = 2 * kWave;
     constexpr int U = 2;
@@ -414,6 +501,7 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
     const int qs = NW / nchunks, rs = NW % nchunks;
     int i = w / nchunks, ch = w % nchunks;
     int ch_pr = -1;
+    bool chunk_special = true;
     dbl2 prs[P];
     for (int64_t u = w; u < units; u += (int64_t)U * NW) {
         int ii[U], cc[U];
@@ -442,46 +530,45 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
             const int j = cc[k] * kChunk + 2 * lane;
             if (cc[k] != ch_pr) {
                 ch_pr = cc[k];
+                chunk_special = !allok;
+                const int c0 = cc[k] * kChunk;
 #pragma unroll
-                for (int q = 0; q < P; ++q)
+                for (int q = 0; q < P; ++q) {
                     prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
                                      : dbl2{0.0, 0.0};
+                    chunk_special = chunk_special || (cq[q] >= c0 && cq[q] < c0 + kChunk);
+                }
             }
             const double* mr = mul + (int64_t)row * kBlkMax;
             double pc[P];
-#pragma unroll
-            for (int q = 0; q < P; ++q) pc[q] = mr[q];
-            dbl2 v = x[k];
+            bool special = chunk_special;
 #pragma unroll
             for (int q = 0; q < P; ++q) {
-                const double e = eq[q], y = yq[q];
-                dbl2 num;
+                pc[q] = mr[q];
+                special = special || row == rq[q];
+            }
+            dbl2 v = x[k];
+            if (!special) {
+                double mn = kFdMaxAbs, mx = 0.0;
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int jj = j + hh;
-                    if (row == rq[q]) {
-                        num[hh] = (jj == cq[q]) ? 1.0 : -v[hh];
-                    } else {
-                        const double a = v[hh] * e;
+                for (int q = 0; q < P; ++q) {
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const double a = v[hh] * eq[q];
                         const double b = prs[q][hh] * pc[q];
-                        num[hh] = (jj == cq[q]) ? v[hh] : (a - b);
+                        const double num = a - b;
+                        mn = fmin(mn, fabs(num));
+                        mx = fmax(mx, fabs(num));
+                        const double t = num * yq[q];          // fd_div inside its window
+                        const double rr = fma(-eq[q], t, num);
+                        v[hh] = fma(rr, yq[q], t);
                     }
                 }
-                // q' = x*y ; r = fma(-e, q', x) ; fma(r, y, q')  (fd_div inside its window)
-                dbl2 out;
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const double t = num[hh] * y;
-                    const double rr = fma(-e, t, num[hh]);
-                    out[hh] = fma(rr, y, t);
-                }
-                const int in = (int)fd_in(num[0]) & (int)fd_in(num[1]);
-                if (!(okq[q] && __all(in))) {
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh)
-                        if (!(okq[q] && fd_in(num[hh]))) out[hh] = num[hh] / e;
-                }
-                v = out;
+                // fmin/fmax skip NaN: a NaN numerator leaves a NaN result, caught by v == v
+                const bool in = mn >= kFdMinAbs && mx < kFdMaxAbs && v[0] == v[0] && v[1] == v[1];
+                if (!__all(in)) v = blk_exact<P>(x[k], row, j, rq, cq, eq, prs, pc);
+            } else {
+                v = blk_exact<P>(v, row, j, rq, cq, eq, prs, pc);
             }
             if (j < C)
                 __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(Tout + (int64_t)row * ld + j));
@@ -517,18 +604,19 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
 }
 
 // End of a block chain: the state of the final table into ctl slot `parity` (first negative
-// "-b" row from the next step's records, entering column from `fr`), like k_publish.
-__global__ __launch_bounds__(kWave) void k_blk_publish(const char* __restrict__ blk,
-                                                       int64_t off_parts, int nparts, int parity,
+// "-b" row from the next step's records, entering column from its cf slot), like k_publish.
+__global__ __launch_bounds__(kWave) void k_blk_publish(const BlkHdr* __restrict__ h,
+                                                       const smx_part* __restrict__ parts,
+                                                       int nparts, int slot, int parity,
                                                        smx_ctl* __restrict__ ctl) {
     if (ctl->term) return;
-    const smx_part* parts = reinterpret_cast<const smx_part*>(blk + off_parts);   // slot 0
+    const smx_part* sp = parts + (int64_t)slot * nparts;
     int nb = SMX_NONE;
-    for (int k = threadIdx.x; k < nparts; k += kWave) nb = min(nb, parts[k].p1col);
+    for (int k = threadIdx.x; k < nparts; k += kWave) nb = min(nb, sp[k].p1col);
     nb = wave_min_int(nb);
     if (threadIdx.x == 0) {
         ctl->negb[parity] = nb;
-        ctl->negf[parity] = reinterpret_cast<const BlkHdr*>(blk)->cf;
+        ctl->negf[parity] = h->cfs[slot];
         ctl->negb[parity ^ 1] = SMX_NONE;
         ctl->negf[parity ^ 1] = SMX_NONE;
     }
