@@ -3,10 +3,13 @@
 Workload (BASELINE.json configs[3], the north-star target config): a 16384 x 16384 dense fp64
 tableau (n = m = 16383; seeded uniform random LP A~U(-1,1), b~U(0.1,1), c~U(-1,1), feasible at
 the origin so the trajectory is a long phase-2 run), resident in HBM before timing starts.
-A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): ONE kernel,
-k_update<kFused> -- the update of step k (recalculate_matrix, :143-177) whose look-ahead
-workgroups also compute step k+1's selection inputs (pick_element, :70-141).  N = 1 times one
-replay of a pre-captured hipGraph of K such kernels.
+A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): its selection
+(pick_element, :70-141) and its Jordan step over every element (recalculate_matrix, :143-177).
+At N = 1 on this table the steps run as block pivots: 8 pivots are decided by one planner launch
+each (k_blk_step, every value of the intermediate tables re-derived from the block's input with
+the update's own expression) and applied by ONE sweep of the tableau (k_blk_sweep), so a sweep
+moves 16 B per element for 8 pivots; bit-identical to one pivot per sweep.  The one-pivot chain
+(k_update<kFused>, one kernel per pivot) is timed beside it as "single_pivot_update".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size S]
 
@@ -15,10 +18,11 @@ constraint rows are block-partitioned (strong scaling of the same tableau) and e
 exchanges one all-gather of (header + candidate rows) over RCCL.  Timing: barrier +
 synchronize on both sides of exactly K pivots, max over ranks.  Rank 0 prints ONE JSON line.
 
-roofline: algorithmic bytes of the update kernel = 16 B per tableau element per pivot
-(read + write every element once), divided by that kernel's average duration measured with
-HIP events on the solver stream inside the timed region (N = 1: events around the graph replay
-/ K, so inter-kernel gaps count as kernel time; N > 1: events around every update kernel).  traffic: HBM bytes per launch from
+roofline: algorithmic bytes of the dominant kernel = 16 B per tableau element per launch
+(read + write every element once; a block sweep applies P pivots per launch), divided by that
+kernel's average duration measured with HIP events on the solver stream inside the timed region
+(block chain: events around every sweep; graph paths: events around the replay / K, so
+inter-kernel gaps count as kernel time; N > 1: events around every update kernel).  traffic: HBM bytes per launch from
 the committed rocprofv3 PMC summary (profiles/), FETCH_SIZE doubled per the gfx950 correction.
 cpu_baseline: the numpy restatement of the same pivot (oracle/numpy_oracle.py, bit-identical to
 the reference) on the same tableau, single thread, a bounded number of pivots.
@@ -184,7 +188,33 @@ def copy_ceiling(nbytes):
     return best
 
 
+def _single_pivot_line(dev, R, C, k):
+    """The one-pivot-per-sweep chain (k_update<kFused>, a hipGraph of k launches) continued from
+    the current table, outside the timed region: the rank-1 update kernel's own roofline."""
+    import torch
+    prev_block = dev.block
+    dev.block = 0
+    try:
+        dev.prepare(k)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(dev.stream)
+        dev.run(k, graph=True)
+        e1.record(dev.stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        dev.sync_state()
+    finally:
+        dev.block = prev_block
+    ach = 16.0 * R * C / (ms * 1e-3 / k) / 1e9
+    return {"kernel": "k_update<kFused>", "pivots_per_launch": 1, "pivots": k,
+            "pivots_s": k / ms * 1e3, "avg_kernel_ms": ms / k, "achieved": ach,
+            "unit": "GB/s", "frac": ach / PEAK_HBM_GBS}
+
+
 def run_single(args):
+    import numpy as np
     import torch
     from simplex_mi355x import _lib, lp
     from simplex_mi355x.device import DeviceTableau
@@ -196,30 +226,70 @@ def run_single(args):
     if args.warmup:
         dev.run(args.warmup, graph=True)
         dev.sync_state()
-    # the timed region replays one pre-captured hipGraph of K chained pivots; HIP events on the
-    # solver stream bracket it, so the kernel average below includes the (tiny) inter-kernel gaps
-    dev.prepare(args.steps)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(dev.stream)
-    dev.run(args.steps, graph=True)
-    ev1.record(dev.stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    dev_ms = ev0.elapsed_time(ev1)
+    resident = dev.resident_plan()
+    bplan = None if resident is not None else dev.block_plan()
+    bytes_per_sweep = 16.0 * R * C   # read + write every element once
+    extra = {}
+    if bplan is not None:
+        # block pivots: P pivots planned from the sweep's input table, then one sweep applies
+        # them all.  The timed region launches the chain eagerly with HIP events around every
+        # sweep on the solver stream (the host stays ahead: ~P+1 launches per ~1.5 ms of work),
+        # so the sweep average comes from the timed run itself.
+        P = bplan[1]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sw, tot_ms = dev.run_block_timed(args.steps, P)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        dev_ms = tot_ms
+        avg_kernel = float(np.mean(sw)) * 1e-3
+        kernel = f"k_blk_sweep<{P}>"
+        traffic = load_traffic(args.traffic, f"{R}x{C}/k_blk_sweep<{P}>")
+        extra = {"pivots_per_launch": P, "launches": len(sw),
+                 "planner_ms_per_pivot": (tot_ms - float(np.sum(sw))) / args.steps,
+                 "algorithmic_bytes_per_pivot": bytes_per_sweep / P}
+        kernels_per_pivot = (P + 1) / P
+    else:
+        # the timed region replays one pre-captured hipGraph of K chained pivots (one fused
+        # k_update per pivot, or the LDS-resident loop for tableaux that fit on chip); HIP events
+        # on the solver stream bracket it, so the kernel average includes the inter-kernel gaps
+        dev.prepare(args.steps)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(dev.stream)
+        dev.run(args.steps, graph=True)
+        ev1.record(dev.stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        dev_ms = ev0.elapsed_time(ev1)
+        avg_kernel = dev_ms * 1e-3 / args.steps   # s per pivot (prime/publish included)
+        if resident is not None:
+            # one launch runs all K pivots: per launch K x 16 B per element, algorithmic only
+            # (the tableau stays in LDS for the whole chain; HBM sees it once in, once out)
+            kernel = "k_resident"
+            avg_kernel = dev_ms * 1e-3
+            bytes_per_sweep *= args.steps
+            extra = {"pivots_per_launch": args.steps,
+                     "note": "tableau held in LDS for the whole chain: the bytes are "
+                             "algorithmic (16 B per element per pivot), not HBM traffic"}
+            kernels_per_pivot = 1.0 / args.steps
+        else:
+            kernel = "k_update<kFused>" if _lib.fused_enabled() else "k_update<kSingle>"
+            kernels_per_pivot = 1 if _lib.fused_enabled() else 2
+            extra = {"pivots_per_launch": 1}
+        traffic = load_traffic(args.traffic, f"{R}x{C}")
     ctl = dev.sync_state()
     done = int(ctl["npivots"])
     valid = done == args.warmup + args.steps and not ctl["term"]
     cycle = cycle_report(n, m, dev.read_log(0, done))
-    bytes_per_pivot = 16.0 * R * C
-    fused = _lib.fused_enabled()   # one k_update<kFused> per pivot, else k_select + k_update
-    avg_upd = dev_ms * 1e-3 / args.steps   # s per pivot kernel (prime/publish included)
-    achieved = bytes_per_pivot / avg_upd / 1e9
+    achieved = bytes_per_sweep / avg_kernel / 1e9
     workload = f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
-    traffic = load_traffic(args.traffic, f"{R}x{C}")
-    copy_gbs = copy_ceiling(16.0 * R * C / 2)   # same bytes as one pivot (outside timing)
+    copy_gbs = copy_ceiling(8.0 * R * C)   # same bytes as one sweep (outside timing)
+    single = None
+    if bplan is not None and valid:
+        single = _single_pivot_line(dev, R, C, 20)
     out = {
         "metric": METRIC,
         "value": args.steps / wall,
@@ -235,15 +305,16 @@ def run_single(args):
         "data": "synthetic: seeded dense random LP generated on the host, uploaded to HBM "
                 "before timing (no dataset)",
         "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
-                   "parallelism": "single GPU", "kernels_per_pivot": 1 if fused else 2},
-        "hbm_gbs_per_pivot": bytes_per_pivot / (wall / args.steps) / 1e9,
+                   "parallelism": "single GPU", "kernels_per_pivot": kernels_per_pivot},
+        "hbm_gbs_per_pivot": 16.0 * R * C / (wall / args.steps) / 1e9,
         "device_ms_per_step": dev_ms / args.steps,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                     "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                     "kernel": "k_update<kFused>" if fused else "k_update<kSingle>",
-                     "algorithmic_bytes_per_launch": bytes_per_pivot,
-                     "avg_kernel_ms": avg_upd * 1e3,
-                     "copy_ceiling_gbs": copy_gbs, "frac_of_copy": achieved / copy_gbs},
+        "roofline": dict({"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                          "kernel": kernel, "algorithmic_bytes_per_launch": bytes_per_sweep,
+                          "avg_kernel_ms": avg_kernel * 1e3,
+                          "copy_ceiling_gbs": copy_gbs, "frac_of_copy": achieved / copy_gbs},
+                         **extra),
+        "single_pivot_update": single,
         "trajectory_valid": bool(valid),
         "basis_cycle": cycle,
     }

@@ -306,8 +306,8 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
  * is in buf[(parity + d) & 1] (the sweep works in place when a block applies an even count).
  * Unsharded tableaux only (row0 = 0, rows = n).  `blk` is device scratch of smx_block_bytes
  * bytes (no initialisation needed).  smx_block_bytes: with *pivots_inout = 0 it asks the
- * library's policy (smx_tune_block: 0 automatic = 4 pivots for tables >= 64 MiB, 1 never, 2..8
- * that many) and returns 0 when chains of `shape` would not use blocks; with 1..8 it asks for
+ * library's policy (smx_tune_block: 0 automatic = 6 pivots for tables of 48..256 MiB, 8
+ * beyond, 1 never, 2..8 that many) and returns 0 when chains of `shape` would not use blocks; with 1..8 it asks for
  * that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
  * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
  * entries) and the chain's total. */

@@ -373,15 +373,20 @@ int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, 
 
 // ---- block pivots (smx_block.hpp) ------------------------------------------------------------
 // smx_tune_block: 0 automatic, 1 never, 2..kBlkMax that many pivots per sweep
+// Automatic policy from tools/block_bench.py (profiles/r01_block_sweep.jsonl): below ~48 MiB the
+// planner's ~15 us per pivot eats the saved traffic (2048^2: block 4 = fused within 1 %); 6
+// pivots per sweep up to 256 MiB (3072^2: 45.8 k pivots/s vs 30.1 k fused), 8 beyond (16384^2).
 int g_block = 0;
-constexpr int kBlockAutoP = 4;
-constexpr int64_t kBlockMinTable = 64ll << 20;
+constexpr int64_t kBlockMinTable = 48ll << 20;
+constexpr int64_t kBlockWideTable = 256ll << 20;
 
 int block_pivots(const smx_shape& s) {
     if (g_block == 1) return 0;
     if (s.row0 != 0 || s.rows != s.n || s.rows < 1 || s.m < 1) return 0;   // unsharded only
     if (g_block >= 2) return g_block;
-    return (int64_t)(s.rows + 1) * s.ld * 8 >= kBlockMinTable ? kBlockAutoP : 0;
+    const int64_t bytes = (int64_t)(s.rows + 1) * s.ld * 8;
+    if (bytes < kBlockMinTable) return 0;
+    return bytes >= kBlockWideTable ? 8 : 6;
 }
 
 using BlkSweepFn = void (*)(double*, double*, int64_t, int, int, const BlkHdr*, const double*,

@@ -187,9 +187,10 @@ def test_block_terminal_state_matches_chain(block_mode):
     assert seen > 10
 
 
-@pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 6, 4), (16383, 16383, 5, 4)])
+@pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 11, 8), (16383, 16383, 9, 8), (3071, 3071, 13, 6)])
 def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
-    """BASELINE sizes through the default policy (4 pivots per sweep), a ragged last block."""
+    """BASELINE sizes through the default policy (6 or 8 pivots per sweep), a ragged last
+    block."""
     from simplex_mi355x import lp, _lib
     from simplex_mi355x.device import DeviceTableau
     from oracle import c_oracle
@@ -210,8 +211,10 @@ def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
 def test_block_plan_policy(block_mode):
     from simplex_mi355x import _lib
     block_mode(0)
-    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 4
-    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4]) is None   # below 64 MiB
+    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 8
+    assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 6
+    assert _lib.block_plan([2048, 2047, 2047, 2047, 2047, 0, 8]) is None    # below 48 MiB
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4]) is None
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 6)[1] == 6
     assert _lib.block_plan([1024, 100, 1023, 1023, 1023, 0, 4], 4) is None  # sharded
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 9) is None

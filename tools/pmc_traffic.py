@@ -1,6 +1,6 @@
 """Derive HBM bytes per launch of the update kernel from two rocprofv3 PMC passes.
 
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY [OUT_JSON]
+usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_KEY [OUT_JSON] [KERNEL_SUBSTRING]
 
 Each pass is `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` (separate runs: on gfx950 the two
 do not fit one pass).  Both counters are in KiB.  gfx950 correction (MI355X_MICROARCH.md §HBM):
@@ -29,12 +29,13 @@ def per_dispatch(d, counter, needle="k_update"):
 def main():
     fdir, wdir, key = sys.argv[1], sys.argv[2], sys.argv[3]
     out = sys.argv[4] if len(sys.argv) > 4 else None
-    f = per_dispatch(fdir, "FETCH_SIZE")
-    w = per_dispatch(wdir, "WRITE_SIZE")
+    needle = sys.argv[5] if len(sys.argv) > 5 else "k_update"
+    f = per_dispatch(fdir, "FETCH_SIZE", needle)
+    w = per_dispatch(wdir, "WRITE_SIZE", needle)
     fetch_kib = statistics.median(f)
     write_kib = statistics.median(w)
     rec = {
-        "kernel": "k_update",
+        "kernel": needle,
         "dispatches": [len(f), len(w)],
         "fetch_size_kib_median": fetch_kib,
         "write_size_kib_median": write_kib,
