@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--traffic", default=None, help="PMC summary json (default: profiles/)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the row-sharded RCCL path even at world size 1")
+    ap.add_argument("--pivots", type=int, default=8,
+                    help="row-sharded path: pivots per sweep (block pivots; 1 = one pivot per "
+                         "sweep, the fused one-pivot protocol)")
     return ap.parse_args()
 
 

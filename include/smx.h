@@ -325,6 +325,41 @@ int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, i
                            int32_t* log, double* xhist, int64_t log_cap, void* stream,
                            void** graph_out);
 
+/* ---- block pivots, row-sharded (one rank per GPU) -----------------------------------------
+ * The block chain of smx_block_run on this rank's row block (shape.row0 / rows; a rank may own
+ * no rows), with ONE all-gather per pivot of the send slots (layout of smx_shard_*: header +
+ * row A + row B, SMX_SHARD_HDR + 2*ld doubles per rank; rows as values of T_{k+D} derived from
+ * the block's input table).  smx_bshard_run issues the all-gathers itself through `comm`
+ * (smx_comm_init) on `stream`; the step-wise calls let a driver do its own exchange:
+ *   prime once per chain; per block `block` = 0, 1, ... (block start parity `parity`), for
+ *   step = 1..pivots: pack(step - 1) -> all-gather send -> recv -> step(step); then sweep(T of
+ *   the block, the other buffer) -- in place for an even count, so the table after d pivots is in
+ *   buf[(parity0 + d) & 1]; after the last block publish(block count).
+ * No x-history on this path (xhist is per-rank); `blk` is smx_bshard_bytes bytes. */
+int64_t smx_bshard_bytes(const smx_shape* shape);
+int smx_bshard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                   int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, double* send,
+                   double* recv, int32_t nranks, void* comm, int32_t* log, int64_t log_cap,
+                   void* stream);
+int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                         int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                         double* send, double* recv, int32_t nranks, void* comm, int32_t* log,
+                         int64_t log_cap, void* stream, float* host_sweep_ms,
+                         float* host_total_ms);
+int smx_bshard_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                     void* blk, int64_t blk_bytes, void* stream);
+int smx_bshard_pack(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
+                    int32_t block, const smx_ctl* ctl, void* blk, int64_t blk_bytes, double* send,
+                    void* stream);
+int smx_bshard_step(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
+                    int32_t parity, int32_t block, const double* recv, int32_t nranks,
+                    smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log, int64_t log_cap,
+                    void* stream);
+int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_t pivots,
+                     void* blk, int64_t blk_bytes, void* stream);
+int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, smx_ctl* ctl,
+                       void* blk, int64_t blk_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

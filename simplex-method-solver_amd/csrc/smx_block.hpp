@@ -211,10 +211,10 @@ __device__ __forceinline__ void blk_rec_store(BlkRec R, smx_part* out) {
     }
 }
 
-// Records of a chain's first step, straight from T (workgroup b of nparts: rows b*NT + tid +
-// q*nparts*NT, the layout of la_partial).
+// Records of a chain's first step, straight from T (workgroup b of nparts: local rows b*NT + tid
+// + q*nparts*NT, the layout of la_partial; global row indices row0 + i in the records).
 __global__ __launch_bounds__(kBlkNT) void k_blk_first(const double* __restrict__ T, int64_t ld,
-                                                      int rows, int m,
+                                                      int rows, int m, int row0,
                                                       const smx_ctl* __restrict__ ctl,
                                                       const BlkHdr* __restrict__ h,
                                                       smx_part* __restrict__ parts) {
@@ -226,25 +226,123 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_first(const double* __restrict__
         const double* row = T + (int64_t)i * ld;
         const double bv = row[m];
         const double a = cf != SMX_NONE ? row[cf] : 0.0;
-        blk_rec_add(R, i, bv, cf != SMX_NONE, a);
+        blk_rec_add(R, row0 + i, bv, cf != SMX_NONE, a);
     }
     blk_rec_store(R, parts + (int64_t)blk_slot(0, 1, 0) * nparts + b);
 }
 
+__device__ __forceinline__ void blk_load_pivots(const BlkHdr* __restrict__ h, int D, BlkPiv* s_pv) {
+    const int t = threadIdx.x;
+    if (t < D) {
+        s_pv->r[t] = h->r[t];
+        s_pv->c[t] = h->c[t];
+        s_pv->e[t] = h->e[t];
+    }
+}
+
+// Row-sharded blocks: this rank's send slot for block step D (layout of k_pack, smx_shard.hpp):
+// the header from its local records of step D, row A = its first ratio candidate when that ratio
+// is NaN (simplex.py:117-121), row B = its first-negative-b row (phase 1) or its best ratio row,
+// both as values of T_{k+D} (chains of length D from the rank's rows of T_k), and hdr[7] = the
+// phase-1 column of row B (simplex.py:81-85) when this rank holds a negative "-b" entry.
+// Workgroup b writes slice b of the rows; workgroup 0 the header.
+template <int D>
+__global__ __launch_bounds__(kBlkNT) void k_bsh_pack(
+    const double* __restrict__ T, int64_t ld, int rows, int m, int row0, int P, int bn,
+    const smx_ctl* __restrict__ ctl, const BlkHdr* __restrict__ h,
+    const smx_part* __restrict__ parts, int nparts, const double* __restrict__ mul,
+    const double* __restrict__ pr, double* __restrict__ send) {
+    constexpr int NT = kBlkNT;
+    __shared__ BlkPiv s_pv;
+    __shared__ int s_tmp[NT / kWave];
+    __shared__ int s_rows[2];
+    __shared__ int s_hi[4];
+    __shared__ double s_hd[2];
+    const int tid = threadIdx.x, b = blockIdx.x, G = gridDim.x;
+    if (ctl->term) return;
+    blk_load_pivots(h, D, &s_pv);
+    if (tid < kWave) {
+        smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
+        const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * nparts;
+        if (tid < nparts) rec = slot[tid];
+        const int nb = wave_min_int(rec.p1col);
+        const First f = wave_first(First{rec.first, rec.first_v});
+        const Cand bb = wave_best(Cand{rec.best_cls, rec.best_i, rec.best_v});
+        if (tid == 0) {
+            s_rows[0] = (f.idx != SMX_NONE && isnan(f.v)) ? f.idx - row0 : -1;
+            s_rows[1] = (nb != SMX_NONE) ? nb - row0 : (bb.cls < 3 ? bb.idx - row0 : -1);
+            s_hi[0] = nb;
+            s_hi[1] = f.idx;
+            s_hi[2] = bb.cls;
+            s_hi[3] = bb.idx;
+            s_hd[0] = f.v;
+            s_hd[1] = bb.v;
+        }
+    }
+    __syncthreads();
+    const int C = m + 1;
+    const int64_t HDR = SMX_SHARD_HDR;
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        const int rl = s_rows[w];
+        if (rl < 0) continue;
+        double mqr[kBlkMax];
+#pragma unroll
+        for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)rl * kBlkMax + q];
+        const int S = ((C + G - 1) / G + 1) & ~1;
+        const int s1 = min(C, (b + 1) * S);
+        double* dst = send + HDR + (int64_t)w * ld;
+        for (int j = b * S + tid; j < s1; j += NT) dst[j] = blk_prv<D>(T, ld, rl, j, s_pv, pr, mqr);
+    }
+    if (b != 0) return;
+    int p1 = SMX_NONE;
+    if (s_hi[0] != SMX_NONE) {
+        // phase 1 on the owner's row: first j < m with T_{k+D}[r][j] > 0, early exit by rounds
+        const int rl = s_rows[1];
+        double mqr[kBlkMax];
+#pragma unroll
+        for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)rl * kBlkMax + q];
+        for (int j0 = 0; j0 < m && p1 == SMX_NONE; j0 += kBlkScan) {
+            int mine = SMX_NONE;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = j0 + k * NT + tid;
+                if (j < m && blk_prv<D>(T, ld, rl, j, s_pv, pr, mqr) > 0.0 && j < mine) mine = j;
+            }
+            p1 = block_min_int<NT>(mine, s_tmp);
+        }
+    }
+    if (tid == 0) {
+        send[0] = (double)s_hi[0];
+        send[1] = (double)s_hi[1];
+        send[2] = s_hd[0];
+        send[3] = (double)s_hi[2];
+        send[4] = (double)s_hi[3];
+        send[5] = s_hd[1];
+        send[6] = (double)h->cfs[blk_slot(D, P, bn)];
+        send[7] = (double)p1;
+    }
+}
+
 // One pivot of the block: decide block step D = L-1 and build the records of step L.
-template <int L>
+// SH = false: the decision from the records of step D and the pivot-row values derived on the
+// fly; SH = true (row-sharded): from the P gathered send slots in `recv` (merge_headers), the
+// pivot row taken from the winning slot.  Pivot rows are LOCAL indices in the header (-1 when
+// another rank owns the row); the log and the labels use global ones.
+template <int L, bool SH>
 __global__ __launch_bounds__(kBlkNT) void k_blk_step(
-    const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int P,
-    int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
+    const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int row0,
+    int P, int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
     smx_part* __restrict__ parts, double* __restrict__ mul, double* __restrict__ pr,
-    double* __restrict__ fr, int32_t* __restrict__ log, double* __restrict__ xhist,
-    int64_t log_cap) {
+    double* __restrict__ fr, const double* __restrict__ recv, int nranks,
+    int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap) {
     constexpr int D = L - 1;
     constexpr int NT = kBlkNT;
     __shared__ BlkPiv s_pv;
     __shared__ int s_tmp[NT / kWave];
     __shared__ Decision s_d;
     __shared__ int s_nb, s_c;
+    __shared__ int64_t s_off;
     __shared__ double s_e, s_fc, s_pm, s_pa;
     const int tid = threadIdx.x;
     const int b = blockIdx.x, G = gridDim.x;
@@ -254,13 +352,20 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
     }
     const int sp = (parity + D) & 1;   // step parity of block step D
     const int C = m + 1;
-    if (tid < D) {
-        s_pv.r[tid] = h->r[tid];
-        s_pv.c[tid] = h->c[tid];
-        s_pv.e[tid] = h->e[tid];
-    }
-    // the decision of step D from its records (every workgroup, identically)
-    if (tid < kWave) {
+    blk_load_pivots(h, D, &s_pv);
+    if (SH) {
+        if (tid == 0) {
+            const ShardDecision sd = merge_headers(recv, nranks, ld, m, flen);
+            int gnb = SMX_NONE;
+            const int64_t slot = SMX_SHARD_HDR + 2 * ld;
+            for (int p = 0; p < nranks; ++p) gnb = min(gnb, (int)recv[p * slot]);
+            s_d = Decision{sd.status, sd.r, sd.c};
+            s_nb = gnb;
+            s_c = (int)recv[6];
+            s_off = sd.off;
+        }
+    } else if (tid < kWave) {
+        // the decision of step D from its records (every workgroup, identically)
         smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
         const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * G;
         if (tid < G) rec = slot[tid];
@@ -312,22 +417,31 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         terminal(d);
         return;
     }
-    const int r = d.r;
+    const int r = d.r;                                   // global pivot row
+    const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
+    const double* prow = SH ? recv + s_off : nullptr;    // T_{k+D}[r][*] (sharded)
     double mqr[kBlkMax];
+    if (!SH) {
 #pragma unroll
-    for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)r * kBlkMax + q];
+        for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)r_local * kBlkMax + q];
+    }
+    auto prv = [&](int j) -> double {
+        if (SH) return prow[j];
+        return blk_prv<D>(T, ld, r_local, j, s_pv, pr, mqr);
+    };
     const double* fo = fr + (int64_t)sp * ld;          // f-row of T_{k+D}
     double* fn = fr + (int64_t)(sp ^ 1) * ld;          // f-row of T_{k+L}
     double* prD = pr + (int64_t)D * ld;
-    if (nb != SMX_NONE) {
+    if (!SH && nb != SMX_NONE) {
         // phase 1: first j < m with T_{k+D}[r][j] > 0 (simplex.py:81-85), early exit by rounds
+        // (sharded: the owner of the row computed it in k_bsh_pack; merge_headers returned it)
         int p1 = SMX_NONE;
         for (int j0 = 0; j0 < m && p1 == SMX_NONE; j0 += kBlkScan) {
             int mine = SMX_NONE;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int j = j0 + k * NT + tid;
-                if (j < m && blk_prv<D>(T, ld, r, j, s_pv, pr, mqr) > 0.0 && j < mine) mine = j;
+                if (j < m && prv(j) > 0.0 && j < mine) mine = j;
             }
             p1 = block_min_int<NT>(mine, s_tmp);
         }
@@ -341,9 +455,9 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
     }
     const int c = d.c;
     if (tid == 0) {
-        s_e = blk_prv<D>(T, ld, r, c, s_pv, pr, mqr);
+        s_e = prv(c);
         s_fc = fo[c];
-        s_pm = blk_prv<D>(T, ld, r, m, s_pv, pr, mqr);
+        s_pm = prv(m);
     }
     __syncthreads();
     const double e = s_e, fc = s_fc;
@@ -352,7 +466,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         const int S = ((C + G - 1) / G + 1) & ~1;
         const int s1 = min(C, (b + 1) * S);
         for (int j = b * S + tid; j < s1; j += NT) {
-            const double v = blk_prv<D>(T, ld, r, j, s_pv, pr, mqr);
+            const double v = prv(j);
             prD[j] = v;
             fn[j] = blk_fnew(fo[j], v, j, c, e, fc);
         }
@@ -364,14 +478,11 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int j = j0 + k * NT + tid;
-            if (j < fscan) {
-                const double v = blk_prv<D>(T, ld, r, j, s_pv, pr, mqr);
-                if (blk_fnew(fo[j], v, j, c, e, fc) < 0.0 && j < mine) mine = j;
-            }
+            if (j < fscan && blk_fnew(fo[j], prv(j), j, c, e, fc) < 0.0 && j < mine) mine = j;
         }
         cf = block_min_int<NT>(mine, s_tmp);
     }
-    if (tid == 0) s_pa = cf != SMX_NONE ? blk_prv<D>(T, ld, r, cf, s_pv, pr, mqr) : 0.0;
+    if (tid == 0) s_pa = cf != SMX_NONE ? prv(cf) : 0.0;
     // the labels after this pivot (simplex.py:152), identically in every workgroup
     const int hx0 = move_label(ctl->xpos[sp][0], r, c);
     const int hx1 = move_label(ctl->xpos[sp][1], r, c);
@@ -379,7 +490,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
     if (b == 0 && tid == 0) {
         const FastDiv fd = fd_prep(e);
         mul[(int64_t)rows * kBlkMax + D] = fc;
-        h->r[D] = r;
+        h->r[D] = r_local;
         h->c[D] = c;
         h->e[D] = e;
         h->y[D] = fd.y;
@@ -406,7 +517,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
     __syncthreads();
     // step L's pivots in LDS-broadcast form: s_pv[D] = this pivot
     if (tid == 0) {
-        s_pv.r[D] = r;
+        s_pv.r[D] = r_local;
         s_pv.c[D] = c;
         s_pv.e[D] = e;
     }
@@ -421,6 +532,9 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         pa_[D] = s_pa;
     }
     const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
+    // x-history of this pivot: the labels' rows as local indices (their "-b" entries of T_{k+L})
+    const int hl0 = hx0 >= row0 && hx0 < row0 + rows ? hx0 - row0 : -1;
+    const int hl1 = hx1 >= row0 && hx1 < row0 + rows ? hx1 - row0 : -1;
     BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
     for (int i = b * NT + tid; i < rows; i += G * NT) {
         const double* row = T + (int64_t)i * ld;
@@ -435,11 +549,11 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         mr[D] = mq[D];
         const double bv = blk_chain<L>(xb, i, m, s_pv, pm_, mq);
         if (xhist && log_cap > 0) {
-            if (i == hx0) xhist[hslot] = bv;
-            if (i == hx1) xhist[hslot + 1] = bv;
+            if (i == hl0) xhist[hslot] = bv;
+            if (i == hl1) xhist[hslot + 1] = bv;
         }
         const double a = cf != SMX_NONE ? blk_chain<L>(xa, i, cf, s_pv, pa_, mq) : 0.0;
-        blk_rec_add(R, i, bv, cf != SMX_NONE, a);
+        blk_rec_add(R, row0 + i, bv, cf != SMX_NONE, a);
     }
     blk_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);
 }

@@ -391,9 +391,12 @@ int block_pivots(const smx_shape& s) {
 
 using BlkSweepFn = void (*)(double*, double*, int64_t, int, int, const BlkHdr*, const double*,
                            const double*);
-using BlkStepFn = void (*)(const double*, int64_t, int, int, int, int, int, int, int, smx_ctl*,
-                           BlkHdr*, smx_part*, double*, double*, double*, int32_t*, double*,
-                           int64_t);
+using BlkStepFn = void (*)(const double*, int64_t, int, int, int, int, int, int, int, int,
+                           smx_ctl*, BlkHdr*, smx_part*, double*, double*, double*, const double*,
+                           int, int32_t*, double*, int64_t);
+using BshPackFn = void (*)(const double*, int64_t, int, int, int, int, int, const smx_ctl*,
+                           const BlkHdr*, const smx_part*, int, const double*, const double*,
+                           double*);
 
 template <bool NTL>
 BlkSweepFn blk_sweep_fn_ntl(int P) {
@@ -409,17 +412,83 @@ BlkSweepFn blk_sweep_fn_ntl(int P) {
     }
 }
 
-BlkStepFn blk_step_fn(int L) {
+template <bool SH>
+BlkStepFn blk_step_fn_sh(int L) {
     switch (L) {
-        case 1: return k_blk_step<1>;
-        case 2: return k_blk_step<2>;
-        case 3: return k_blk_step<3>;
-        case 4: return k_blk_step<4>;
-        case 5: return k_blk_step<5>;
-        case 6: return k_blk_step<6>;
-        case 7: return k_blk_step<7>;
-        default: return k_blk_step<8>;
+        case 1: return k_blk_step<1, SH>;
+        case 2: return k_blk_step<2, SH>;
+        case 3: return k_blk_step<3, SH>;
+        case 4: return k_blk_step<4, SH>;
+        case 5: return k_blk_step<5, SH>;
+        case 6: return k_blk_step<6, SH>;
+        case 7: return k_blk_step<7, SH>;
+        default: return k_blk_step<8, SH>;
     }
+}
+
+BshPackFn bsh_pack_fn(int D) {
+    switch (D) {
+        case 0: return k_bsh_pack<0>;
+        case 1: return k_bsh_pack<1>;
+        case 2: return k_bsh_pack<2>;
+        case 3: return k_bsh_pack<3>;
+        case 4: return k_bsh_pack<4>;
+        case 5: return k_bsh_pack<5>;
+        case 6: return k_bsh_pack<6>;
+        default: return k_bsh_pack<7>;
+    }
+}
+
+// Scratch pointers of a block chain
+struct BlkPtrs {
+    BlkLayout L;
+    BlkHdr* h;
+    smx_part* parts;
+    double *mul, *pr, *fr;
+};
+BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
+    BlkPtrs b;
+    b.L = blk_layout(s.rows + 1, s.ld, s.nparts);
+    b.h = reinterpret_cast<BlkHdr*>(blk);
+    b.parts = reinterpret_cast<smx_part*>(blk + b.L.parts);
+    b.mul = reinterpret_cast<double*>(blk + b.L.mul);
+    b.pr = reinterpret_cast<double*>(blk + b.L.pr);
+    b.fr = reinterpret_cast<double*>(blk + b.L.fr);
+    return b;
+}
+
+int launch_blk_prime(const double* T, const smx_shape& s, int parity, smx_ctl* ctl,
+                     const BlkPtrs& b, hipStream_t st) {
+    hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, T, s.ld, s.rows, s.m,
+                       fscan_of(s), parity, (const smx_ctl*)ctl, b.h, b.fr);
+    hipLaunchKernelGGL(k_blk_first, dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
+                       s.row0, (const smx_ctl*)ctl, (const BlkHdr*)b.h, b.parts);
+    return (int)hipGetLastError();
+}
+
+int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, int parity,
+                    int bn, smx_ctl* ctl, const BlkPtrs& b, const double* recv, int nranks,
+                    int32_t* log, double* xhist, int64_t log_cap, hipStream_t st) {
+    BlkStepFn fn = sh ? blk_step_fn_sh<true>(L) : blk_step_fn_sh<false>(L);
+    hipLaunchKernelGGL(fn, dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
+                       fscan_of(s), s.row0, P, parity, bn, ctl, b.h, b.parts, b.mul, b.pr, b.fr,
+                       recv, nranks, log, xhist, log_cap);
+    return (int)hipGetLastError();
+}
+
+int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
+                    const smx_ctl* ctl, const BlkPtrs& b, double* send, hipStream_t st) {
+    hipLaunchKernelGGL(bsh_pack_fn(D), dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
+                       s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h, (const smx_part*)b.parts,
+                       s.nparts, (const double*)b.mul, (const double*)b.pr, send);
+    return (int)hipGetLastError();
+}
+
+int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, const BlkPtrs& b,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)b.h,
+                       (const smx_part*)b.parts, s.nparts, blk_slot(0, 1, bn), parity, ctl);
+    return (int)hipGetLastError();
 }
 
 int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, char* blk,
@@ -435,50 +504,57 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
 }
 
 // k pivots in blocks of P: prime + first records, then per block P step launches and one sweep;
-// publish.  ev (optional): 2 events per block recorded around its sweep.
+// publish.  ev (optional): 2 events per block recorded around its sweep.  With comm (row-sharded,
+// one rank per GPU): every step launch is preceded by this rank's pack and ONE ncclAllGather of
+// the send slots into recv, on the same stream.
 int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parity, int k, int P,
                        smx_ctl* ctl, char* blk, int32_t* log, double* xhist, int64_t log_cap,
-                       hipStream_t st, hipEvent_t* ev = nullptr) {
-    const BlkLayout L = blk_layout(s.rows + 1, s.ld, s.nparts);
-    BlkHdr* h = reinterpret_cast<BlkHdr*>(blk);
-    smx_part* parts = reinterpret_cast<smx_part*>(blk + L.parts);
-    double* mul = reinterpret_cast<double*>(blk + L.mul);
-    double* pr = reinterpret_cast<double*>(blk + L.pr);
-    double* fr = reinterpret_cast<double*>(blk + L.fr);
-    const int fscan = fscan_of(s);
-    const double* t0 = parity ? buf1 : buf0;
-    hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, t0, s.ld, s.rows, s.m, fscan,
-                       parity, (const smx_ctl*)ctl, h, fr);
-    hipLaunchKernelGGL(k_blk_first, dim3(s.nparts), dim3(kBlkNT), 0, st, t0, s.ld, s.rows, s.m,
-                       (const smx_ctl*)ctl, (const BlkHdr*)h, parts);
-    int err = (int)hipGetLastError();
+                       hipStream_t st, hipEvent_t* ev = nullptr, double* send = nullptr,
+                       double* recv = nullptr, int nranks = 0, ncclComm_t comm = nullptr) {
+    const BlkPtrs bp = blk_ptrs(s, blk);
+    const bool sh = comm != nullptr;
+    const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)s.ld;
+    int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, ctl, bp, st);
     int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
         const int Pb = (k - done < P) ? k - done : P;
         double* tin = p ? buf1 : buf0;
         double* toth = p ? buf0 : buf1;
-        for (int l = 1; l <= Pb; ++l)
-            hipLaunchKernelGGL(blk_step_fn(l), dim3(s.nparts), dim3(kBlkNT), 0, st,
-                               (const double*)tin, s.ld, s.rows, s.m, s.flen, fscan, Pb, p, bn,
-                               ctl, h, parts, mul, pr, fr, log, xhist, log_cap);
-        err = (int)hipGetLastError();
+        for (int l = 1; l <= Pb && !err; ++l) {
+            if (sh) {
+                err = launch_bsh_pack(l - 1, tin, s, Pb, bn, ctl, bp, send, st);
+                if (!err) {
+                    const ncclResult_t r = ncclAllGather(send, recv, slot, ncclFloat64, comm, st);
+                    if (r != ncclSuccess) err = -1000 - (int)r;
+                }
+            }
+            if (!err)
+                err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
+                                      sh ? nullptr : xhist, log_cap, st);
+        }
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
-        if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, L, st);
+        if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st);
         if (ev) (void)hipEventRecord(ev[2 * bn + 1], st);
         p = (p + Pb) & 1;
         done += Pb;
         ++bn;
     }
     if (err) return err;
-    hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)h,
-                       (const smx_part*)parts, s.nparts, blk_slot(0, 1, bn), p, ctl);
-    return (int)hipGetLastError();
+    return launch_blk_publish(s, p, bn, ctl, bp, st);
 }
 
 bool block_args_ok(const smx_shape* shape, int k, int P, const void* blk, int64_t blk_bytes) {
     if (!shape_ok(shape) || k < 0 || P < 1 || P > kBlkMax || !blk) return false;
     const smx_shape& s = *shape;
     if (s.row0 != 0 || s.rows != s.n || s.rows < 1 || s.m < 1) return false;
+    return blk_bytes >= blk_layout(s.rows + 1, s.ld, s.nparts).bytes;
+}
+
+// row-sharded blocks: any row block (a rank may own no rows), one f-row replica per rank
+bool bshard_args_ok(const smx_shape* shape, int P, const void* blk, int64_t blk_bytes) {
+    if (!shape_ok(shape) || P < 1 || P > kBlkMax || !blk) return false;
+    const smx_shape& s = *shape;
+    if (s.rows < 0 || s.n < 1 || s.m < 1 || s.row0 < 0 || s.row0 + s.rows > s.n) return false;
     return blk_bytes >= blk_layout(s.rows + 1, s.ld, s.nparts).bytes;
 }
 
@@ -1212,6 +1288,104 @@ int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, i
     }
     *graph_out = g;
     return 0;
+}
+
+int64_t smx_bshard_bytes(const smx_shape* shape) {
+    if (!bshard_args_ok(shape, 1, shape, INT64_MAX)) return 0;
+    return blk_layout(shape->rows + 1, shape->ld, shape->nparts).bytes;
+}
+
+int smx_bshard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
+                   int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, double* send,
+                   double* recv, int32_t nranks, void* comm, int32_t* log, int64_t log_cap,
+                   void* stream) {
+    if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || !send ||
+        !recv || nranks < 1 || !comm || k < 0)
+        return (int)hipErrorInvalidValue;
+    if (k == 0) return 0;
+    return launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                              static_cast<char*>(blk), log, nullptr, log_cap, S(stream), nullptr,
+                              send, recv, nranks, reinterpret_cast<ncclComm_t>(comm));
+}
+
+int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                         int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                         double* send, double* recv, int32_t nranks, void* comm, int32_t* log,
+                         int64_t log_cap, void* stream, float* host_sweep_ms,
+                         float* host_total_ms) {
+    if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || !send ||
+        !recv || nranks < 1 || !comm || k < 1 || !host_sweep_ms || !host_total_ms)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    const int nb = (k + pivots - 1) / pivots;
+    hipEvent_t* ev = new hipEvent_t[2 * (size_t)nb + 2];
+    for (int i = 0; i < 2 * nb + 2; ++i) {
+        if (hipEventCreate(&ev[i]) != hipSuccess) {
+            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
+            delete[] ev;
+            return (int)hipErrorOutOfMemory;
+        }
+    }
+    (void)hipEventRecord(ev[2 * nb], st);
+    int err = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                                 static_cast<char*>(blk), log, nullptr, log_cap, st, ev, send,
+                                 recv, nranks, reinterpret_cast<ncclComm_t>(comm));
+    (void)hipEventRecord(ev[2 * nb + 1], st);
+    if (!err) err = (int)hipEventSynchronize(ev[2 * nb + 1]);
+    if (!err) {
+        for (int b = 0; b < nb; ++b)
+            (void)hipEventElapsedTime(&host_sweep_ms[b], ev[2 * b], ev[2 * b + 1]);
+        (void)hipEventElapsedTime(host_total_ms, ev[2 * nb], ev[2 * nb + 1]);
+    }
+    for (int i = 0; i < 2 * nb + 2; ++i) (void)hipEventDestroy(ev[i]);
+    delete[] ev;
+    return err;
+}
+
+int smx_bshard_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
+                     void* blk, int64_t blk_bytes, void* stream) {
+    if (!bshard_args_ok(shape, 1, blk, blk_bytes) || !ctl) return (int)hipErrorInvalidValue;
+    return launch_blk_prime(T, *shape, parity & 1, ctl, blk_ptrs(*shape, static_cast<char*>(blk)),
+                            S(stream));
+}
+
+int smx_bshard_pack(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
+                    int32_t block, const smx_ctl* ctl, void* blk, int64_t blk_bytes, double* send,
+                    void* stream) {
+    if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || !ctl || !send || step < 0 ||
+        step >= pivots || block < 0)
+        return (int)hipErrorInvalidValue;
+    return launch_bsh_pack(step, T, *shape, pivots, block, ctl,
+                           blk_ptrs(*shape, static_cast<char*>(blk)), send, S(stream));
+}
+
+int smx_bshard_step(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
+                    int32_t parity, int32_t block, const double* recv, int32_t nranks,
+                    smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log, int64_t log_cap,
+                    void* stream) {
+    if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || !ctl || !recv || nranks < 1 ||
+        step < 1 || step > pivots || block < 0)
+        return (int)hipErrorInvalidValue;
+    return launch_blk_step(true, step, T, *shape, pivots, parity & 1, block, ctl,
+                           blk_ptrs(*shape, static_cast<char*>(blk)), recv, nranks, log, nullptr,
+                           log_cap, S(stream));
+}
+
+int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_t pivots,
+                     void* blk, int64_t blk_bytes, void* stream) {
+    if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || Tin == Tother)
+        return (int)hipErrorInvalidValue;
+    const BlkPtrs bp = blk_ptrs(*shape, static_cast<char*>(blk));
+    return launch_block_sweep(Tin, Tother, *shape, pivots, static_cast<char*>(blk), bp.L,
+                              S(stream));
+}
+
+int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, smx_ctl* ctl,
+                       void* blk, int64_t blk_bytes, void* stream) {
+    if (!bshard_args_ok(shape, 1, blk, blk_bytes) || !ctl || block < 0)
+        return (int)hipErrorInvalidValue;
+    return launch_blk_publish(*shape, parity & 1, block, ctl,
+                              blk_ptrs(*shape, static_cast<char*>(blk)), S(stream));
 }
 
 }  // extern "C"

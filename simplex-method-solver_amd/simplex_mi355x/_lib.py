@@ -54,6 +54,8 @@ EXPORTS = (
     "smx_resident_run", "smx_fastdiv_check",
     "smx_tune_block", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_graph_create",
+    "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
+    "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
 )
 
 
@@ -131,6 +133,18 @@ def load():
                                 ctypes.c_int),
         "smx_block_graph_create": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp,
                                     ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+        "smx_bshard_bytes": ([sp], ctypes.c_int64),
+        "smx_bshard_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, i64,
+                            vp], ctypes.c_int),
+        "smx_bshard_run_timed": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp,
+                                  i64, vp, ctypes.POINTER(ctypes.c_float),
+                                  ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "smx_bshard_prime": ([vp, sp, i32, vp, vp, i64, vp], ctypes.c_int),
+        "smx_bshard_pack": ([vp, sp, i32, i32, i32, vp, vp, i64, vp, vp], ctypes.c_int),
+        "smx_bshard_step": ([vp, sp, i32, i32, i32, i32, vp, i32, vp, vp, i64, vp, i64, vp],
+                            ctypes.c_int),
+        "smx_bshard_sweep": ([vp, vp, sp, i32, vp, i64, vp], ctypes.c_int),
+        "smx_bshard_publish": ([sp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -219,6 +219,137 @@ class HipShardBackend:
         return self.dev.download()
 
 
+class BlockShardBackend:
+    """This rank's row block for BLOCK pivots (smx_bshard_*, csrc/smx_block.hpp): per pivot the
+    rank packs its header + candidate rows as values of T_{k+D} derived from the block's input,
+    one all-gather exchanges the slots (the layout of the one-pivot protocol above), and the step
+    kernel merges them, records the pivot and prepares the next step; every ``pivots`` pivots
+    ONE sweep applies them all to the rank's rows.  Same methods for the numpy mirror of the
+    gloo tests (tests/shard_numpy_backend.py, NumpyBlockShardBackend)."""
+
+    def __init__(self, local_T: np.ndarray, n: int, m: int, flen: int, row0: int, world: int,
+                 device=None, log_cap: int = 1 << 16, pivots: int = 8):
+        self.dev = DeviceTableau(local_T, n, m, flen, device=device, row0=row0, n_global=n,
+                                 log_cap=log_cap, block=0)
+        self.world = world
+        self.pivots = int(pivots)
+        self.slot = ops.shard_slot(self.dev.ld)
+        self._shape = ops.make_shape(self.dev.shape)
+        nbytes = int(_lib.load().smx_bshard_bytes(ctypes.byref(self._shape)))
+        if nbytes <= 0:
+            raise ValueError(f"shape {self.dev.shape} is not eligible for sharded block pivots")
+        with torch.cuda.stream(self.dev.stream):
+            self.send = torch.zeros(self.slot, dtype=torch.float64, device=self.dev.device)
+            self.recv = torch.zeros(world * self.slot, dtype=torch.float64,
+                                    device=self.dev.device)
+            self.blk = torch.zeros((nbytes + 7) // 8, dtype=torch.int64, device=self.dev.device)
+        self._nbytes = nbytes
+
+    def stream_ctx(self):
+        return torch.cuda.stream(self.dev.stream)
+
+    # -- the step-wise protocol (include/smx.h, smx_bshard_*) ---------------------------------
+    def parity(self) -> int:
+        return self.dev.step & 1
+
+    def prime(self) -> None:
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_prime(
+            d.buf[d.step & 1].data_ptr(), ctypes.byref(self._shape), d.step & 1,
+            d.ctl.data_ptr(), self.blk.data_ptr(), self._nbytes, d.stream.cuda_stream),
+            "smx_bshard_prime")
+
+    def pack(self, step: int, pivots: int, block: int, parity: int) -> None:
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_pack(
+            d.buf[parity].data_ptr(), ctypes.byref(self._shape), step, pivots, block,
+            d.ctl.data_ptr(), self.blk.data_ptr(), self._nbytes, self.send.data_ptr(),
+            d.stream.cuda_stream), "smx_bshard_pack")
+
+    def decide(self, step: int, pivots: int, parity: int, block: int) -> None:
+        """smx_bshard_step: merge the gathered slots, record pivot ``step - 1`` of the block,
+        prepare step ``step``."""
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_step(
+            d.buf[parity].data_ptr(), ctypes.byref(self._shape), step, pivots, parity, block,
+            self.recv.data_ptr(), self.world, d.ctl.data_ptr(), self.blk.data_ptr(),
+            self._nbytes, d.log.data_ptr(), d.log_cap, d.stream.cuda_stream), "smx_bshard_step")
+
+    def sweep(self, pivots: int, parity: int) -> None:
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_sweep(
+            d.buf[parity].data_ptr(), d.buf[parity ^ 1].data_ptr(), ctypes.byref(self._shape),
+            pivots, self.blk.data_ptr(), self._nbytes, d.stream.cuda_stream), "smx_bshard_sweep")
+        d.step += pivots
+        d._pending = True
+
+    def publish(self, parity: int, block: int) -> None:
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_publish(
+            ctypes.byref(self._shape), parity, block, d.ctl.data_ptr(), self.blk.data_ptr(),
+            self._nbytes, d.stream.cuda_stream), "smx_bshard_publish")
+
+    # -- the native chain (libsmx issues the all-gathers) -------------------------------------
+    def run_native(self, k: int, comm: "RcclComm") -> None:
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_run(
+            d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
+            self.pivots, d.ctl.data_ptr(), self.blk.data_ptr(), self._nbytes,
+            self.send.data_ptr(), self.recv.data_ptr(), self.world, comm.handle,
+            d.log.data_ptr(), d.log_cap, d.stream.cuda_stream), "smx_bshard_run")
+        d.step += k
+        d._pending = True
+
+    def run_native_timed(self, k: int, comm: "RcclComm"):
+        """Like run_native, with HIP events around every sweep (synchronous)."""
+        d = self.dev
+        nb = -(-k // self.pivots)
+        sw = (ctypes.c_float * nb)()
+        tot = ctypes.c_float()
+        _lib.check(_lib.load().smx_bshard_run_timed(
+            d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
+            self.pivots, d.ctl.data_ptr(), self.blk.data_ptr(), self._nbytes,
+            self.send.data_ptr(), self.recv.data_ptr(), self.world, comm.handle,
+            d.log.data_ptr(), d.log_cap, d.stream.cuda_stream, sw, ctypes.byref(tot)),
+            "smx_bshard_run_timed")
+        d.step += k
+        d._pending = True
+        return np.frombuffer(sw, dtype=np.float32).copy(), float(tot.value)
+
+    def state(self) -> dict:
+        c = self.dev.sync_state()
+        return {"npivots": int(c["npivots"]), "term": bool(c["term"]),
+                "status": int(c["sel_status"]), "r": int(c["sel_r"]), "c": int(c["sel_c"])}
+
+    def log(self, start: int, stop: int) -> np.ndarray:
+        return self.dev.read_log(start, stop)
+
+    def local_table(self) -> np.ndarray:
+        return self.dev.download()
+
+
+def run_block_protocol(be, k: int, exchange, pivots: int | None = None) -> None:
+    """k pivots of the block protocol on one rank's backend with any exchange (``exchange()``
+    all-gathers ``be.send`` into ``be.recv``): prime; per block of P pivots, P times pack ->
+    exchange -> step, then one sweep; publish.  Stream-ordered, no host synchronisation."""
+    P = int(pivots if pivots is not None else be.pivots)
+    with be.stream_ctx():
+        be.prime()
+        parity = be.parity()
+        done = bn = 0
+        while done < k:
+            pb = min(P, k - done)
+            for step in range(1, pb + 1):
+                be.pack(step - 1, pb, bn, parity)
+                exchange()
+                be.decide(step, pb, parity, bn)
+            be.sweep(pb, parity)
+            parity = (parity + pb) & 1
+            done += pb
+            bn += 1
+        be.publish(parity, bn)
+
+
 class ShardedSolver:
     """The per-pivot protocol over any backend with begin/finish/state and a send/recv pair.
 
@@ -273,18 +404,27 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     local = np.zeros((hi - lo + 1, m + 1), dtype=np.float64)
     local[:-1] = lp.dense_rows(args.kind, args.seed, n, m, lo, hi)
     local[-1, :m] = lp.objective(args.kind, args.seed, m)
-    be = HipShardBackend(local, n, m, m, lo, world, device=device,
-                         log_cap=max(1 << 16, args.warmup + args.steps))
+    pivots = int(getattr(args, "pivots", 8) or 1)
+    block = pivots > 1
+    if block:
+        be = BlockShardBackend(local, n, m, m, lo, world, device=device,
+                               log_cap=max(1 << 16, args.warmup + args.steps), pivots=pivots)
+    else:
+        be = HipShardBackend(local, n, m, m, lo, world, device=device,
+                             log_cap=max(1 << 16, args.warmup + args.steps))
     del local
     comm = RcclComm()
-    solver = ShardedSolver(be, comm=comm)
     if args.warmup:
-        solver.run(args.warmup)
+        if block:
+            be.run_native(args.warmup, comm)
+        else:
+            ShardedSolver(be, comm=comm).run(args.warmup)
+        be.state()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    upd_ms, _ = be.run_native_timed(args.steps, comm)
+    upd_ms, tot_ms = be.run_native_timed(args.steps, comm)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -330,17 +470,24 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
             "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
                        "parallelism": f"row-shard x{world} (1 RCCL all-gather per pivot, "
                                       "issued natively on the solver stream)",
-                       "rows_per_rank": hi - lo, "kernels_per_pivot": 2 if be.fused else 3,
-                       "gather_overlapped_with_sweep": be.overlap,
+                       "rows_per_rank": hi - lo,
+                       "pivots_per_sweep": pivots if block else 1,
+                       "kernels_per_pivot": (2 * pivots + 1) / pivots if block
+                       else (2 if be.fused else 3),
+                       "gather_overlapped_with_sweep": False if block else be.overlap,
                        "collectives_per_pivot": 1},
             "hbm_gbs_per_pivot": 16.0 * R * C / (wall / args.steps) / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak_gbs, "unit": "GB/s",
                          "frac": achieved / peak_gbs, "traffic": traffic,
-                         "kernel": ("k_update<kShardFused>" if be.fused else "k_update<kShard>")
+                         "kernel": (f"k_blk_sweep<{pivots}>" if block else
+                                    ("k_update<kShardFused>" if be.fused else "k_update<kShard>"))
                                    + " (rank 0)",
+                         "pivots_per_launch": pivots if block else 1,
                          "algorithmic_bytes_per_launch": local_bytes,
                          "avg_kernel_ms": avg_upd * 1e3,
-                         "max_rank_avg_kernel_ms": float(mx[1])},
+                         "max_rank_avg_kernel_ms": float(mx[1]),
+                         "planner_exchange_ms_per_pivot":
+                             (tot_ms - float(upd_ms.sum())) / args.steps},
             "trajectory_valid": bool(mn[2] > 0.5),
             "basis_cycle": cycle,
             "cpu_baseline": None,

@@ -155,3 +155,37 @@ class NumpyShardBackend:
 
     def local_table(self):
         return self.T[:, :self.C].copy()
+
+
+class NumpyBlockShardBackend(NumpyShardBackend):
+    """CPU stand-in for sharded.BlockShardBackend.  The block protocol exchanges the same slots
+    as the one-pivot protocol (header + rows A / B as values of T_{k+D}); the HIP kernels derive
+    those rows from the block's input table by chains of the update expression, this mirror by
+    keeping its rows materialised after every pivot -- the same values -- so pack is begin(),
+    decide is finish(), and the sweep has nothing left to do."""
+
+    def __init__(self, *args, pivots=8, **kw):
+        super().__init__(*args, **kw)
+        self.P = pivots          # (self.pivots is the mirror's pivot log)
+        self.calls = []
+
+    def parity(self):
+        return self.step & 1
+
+    def prime(self):
+        self.calls.append(("prime",))
+
+    def pack(self, step, pivots, block, parity):
+        assert parity == (self.step - step) & 1, "pack on the block's input parity"
+        self.calls.append(("pack", step, pivots, block))
+        self.begin()
+
+    def decide(self, step, pivots, parity, block):
+        self.calls.append(("decide", step, pivots, block))
+        self.finish()
+
+    def sweep(self, pivots, parity):
+        self.calls.append(("sweep", pivots, parity))
+
+    def publish(self, parity, block):
+        self.calls.append(("publish", parity, block))

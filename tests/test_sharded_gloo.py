@@ -121,3 +121,75 @@ def test_sharded_nan_first_local_but_not_global(tmp_path):
     T[n, :m] = [-1, -1]
     _run(tmp_path, T, n, m, 1, 2)
     _compare(tmp_path, T, n, m, 1)
+
+
+# ---------------------------------------------------------------------------------------------
+# block protocol (sharded.run_block_protocol, the driver of smx_bshard_*): pack -> all-gather
+# -> decide per pivot, one sweep per block of P, publish -- over gloo with the numpy mirror
+def _block_worker(rank, world, port, case, outdir):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    for p in (repo, os.path.join(repo, "simplex-method-solver_amd"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    from shard_numpy_backend import NumpyBlockShardBackend
+    from simplex_mi355x.sharded import row_range, run_block_protocol
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    T = np.load(os.path.join(outdir, "T.npy"))
+    n, m, k, P = case["n"], case["m"], case["k"], case["P"]
+    lo, hi = row_range(n, rank, world)
+    local = np.concatenate([T[lo:hi], T[n:n + 1]], axis=0)
+    be = NumpyBlockShardBackend(local, n, m, m, lo, world, pivots=P)
+    done = 0
+    for chunk in case["chunks"]:
+        run_block_protocol(be, chunk, lambda: dist.all_gather_into_tensor(be.recv, be.send),
+                           pivots=P)
+        done += chunk
+    st = be.state()
+    gathered = [None] * world
+    dist.all_gather_object(gathered, be.local_table()[:-1].copy())
+    if rank == 0:
+        full = np.concatenate(gathered + [be.local_table()[-1:]], axis=0)
+        np.save(os.path.join(outdir, "out.npy"), full)
+        with open(os.path.join(outdir, "out.json"), "w") as fh:
+            json.dump({"state": st, "log": be.log(0, st["npivots"]).tolist(),
+                       "calls": be.calls}, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,n,m,world,P,chunks", [
+    ("uniform", 64, 48, 2, 8, [20, 13]),
+    ("mixed", 47, 33, 3, 3, [7, 30]),
+    ("degenerate_mixed", 45, 25, 2, 5, [60]),
+    ("mixed", 2, 6, 3, 4, [9, 9]),        # rank 0 owns no rows
+])
+def test_block_protocol_matches_oracle(tmp_path, kind, n, m, world, P, chunks):
+    T = _case_T(kind, n, m, 3)
+    np.save(tmp_path / "T.npy", T)
+    k = sum(chunks)
+    case = {"n": n, "m": m, "k": k, "P": P, "chunks": chunks}
+    mp.spawn(_block_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world,
+             join=True)
+    _compare(tmp_path, T, n, m, k)
+    calls = json.load(open(tmp_path / "out.json"))["calls"]
+    # per chunk: prime, then blocks of P (last one ragged) of pack/decide pairs, sweep, publish
+    exp = []
+    for chunk in chunks:
+        exp.append(["prime"])
+        done = bn = 0
+        while done < chunk:
+            pb = min(P, chunk - done)
+            for step in range(1, pb + 1):
+                exp += [["pack", step - 1, pb, bn], ["decide", step, pb, bn]]
+            exp.append(["sweep", pb, None])
+            done += pb
+            bn += 1
+        exp.append(["publish", None, bn])
+    got = [[c[0]] + [None if (c[0], i) in (("sweep", 2), ("publish", 1)) else x
+                     for i, x in enumerate(c[1:], 1)] for c in calls]
+    assert got == exp
