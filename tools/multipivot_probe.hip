@@ -230,6 +230,265 @@ __global__ __launch_bounds__(kBlock) void k_multi2(const double* __restrict__ Ti
     }
 }
 
+// Variant 3 (smx_block.hpp's sweep): fast path with the smallest / largest |numerator| tracked
+// per lane and one wave vote per unit; PF: the next batch's loads issued before the arithmetic.
+constexpr double kMinAbs = 0x1p-127, kMaxAbs = 0x1p130;
+template <int P, bool PF>
+__global__ __launch_bounds__(kBlock) void k_multi3(const double* __restrict__ Tin,
+                                                    double* Tout, int64_t ld, int R, int C,
+                                                    const double* __restrict__ PR,
+                                                    const double* __restrict__ M, Piv pv) {
+    const int lane = threadIdx.x & 63;
+    const int NW = gridDim.x * kWaves;
+    const int w = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunks = (C + kChunk - 1) / kChunk;
+    const int64_t units = (int64_t)nchunks * R;
+    const int qs = NW / nchunks, rs = NW % nchunks;
+    int i = w / nchunks, ch = w % nchunks;
+    int ch_pr = -1;
+    bool cspecial = true;
+    dbl2 pr[P];
+    constexpr int U = 2;
+    struct Bt {
+        int ii[U], cc[U];
+        dbl2 x[U];
+    };
+    auto fetch = [&](Bt& bt) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            bt.ii[k] = i;
+            bt.cc[k] = ch;
+            ch += rs;
+            i += qs;
+            if (ch >= nchunks) {
+                ch -= nchunks;
+                ++i;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int j = bt.cc[k] * kChunk + 2 * lane;
+            bt.x[k] = dbl2{0.0, 0.0};
+            if (bt.ii[k] < R && j < C)
+                bt.x[k] = __builtin_nontemporal_load(
+                    reinterpret_cast<const dbl2*>(Tin + (int64_t)bt.ii[k] * ld + j));
+        }
+    };
+    Bt cur;
+    if (PF && w < units) fetch(cur);
+    for (int64_t u = w; u < units; u += (int64_t)U * NW) {
+        Bt nxt;
+        if (PF) {
+            if (u + (int64_t)U * NW < units) fetch(nxt);
+        } else {
+            fetch(cur);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int row = cur.ii[k];
+            if (row >= R) continue;
+            const int j = cur.cc[k] * kChunk + 2 * lane;
+            if (cur.cc[k] != ch_pr) {
+                ch_pr = cur.cc[k];
+                cspecial = false;
+                const int c0 = cur.cc[k] * kChunk;
+#pragma unroll
+                for (int l = 0; l < P; ++l) {
+                    pr[l] = (j < C) ? *reinterpret_cast<const dbl2*>(PR + (int64_t)l * ld + j)
+                                    : dbl2{0.0, 0.0};
+                    cspecial = cspecial || (pv.c[l] >= c0 && pv.c[l] < c0 + kChunk);
+                }
+            }
+            double pc[P];
+            bool special = cspecial;
+#pragma unroll
+            for (int l = 0; l < P; ++l) {
+                pc[l] = M[(int64_t)row * kMaxP + l];
+                special = special || row == pv.r[l];
+            }
+            dbl2 v = cur.x[k];
+            if (!special) {
+                double mn = kMaxAbs, mx = 0.0;
+#pragma unroll
+                for (int l = 0; l < P; ++l) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const double num = v[h] * pv.e[l] - pr[l][h] * pc[l];
+                        mn = fmin(mn, fabs(num));
+                        mx = fmax(mx, fabs(num));
+                        const double t = num * pv.y[l];
+                        const double rr = fma(-pv.e[l], t, num);
+                        v[h] = fma(rr, pv.y[l], t);
+                    }
+                }
+                const bool in = mn >= kMinAbs && mx < kMaxAbs && v[0] == v[0] && v[1] == v[1];
+                if (!__all(in)) v = chain_exact<P>(cur.x[k], row, j, pv, pr, pc);
+            } else {
+                v = chain_exact<P>(v, row, j, pv, pr, pc);
+            }
+            if (j < C)
+                __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(Tout + (int64_t)row * ld + j));
+        }
+        if (PF) cur = nxt;
+    }
+}
+
+template <int P, bool PF>
+float run3(const double* a, double* b, int64_t ld, int R, int C, const double* PR, const double* M,
+           const Piv& pv, int grid, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    hipLaunchKernelGGL((k_multi3<P, PF>), dim3(grid), dim3(kBlock), 0, 0, a, b, ld, R, C, PR, M, pv);
+    CK(hipEventRecord(e0));
+    for (int t = 0; t < reps; ++t)
+        hipLaunchKernelGGL((k_multi3<P, PF>), dim3(grid), dim3(kBlock), 0, 0, a, b, ld, R, C, PR,
+                           M, pv);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / reps;
+}
+
+template <int P>
+void row3(int R, const double* a, double* b, int64_t ld, int C, const double* PR, const double* M,
+          const Piv& pv, int cus, int reps) {
+    hipFuncAttributes fa0, fa1;
+    CK(hipFuncGetAttributes(&fa0, (const void*)k_multi3<P, false>));
+    CK(hipFuncGetAttributes(&fa1, (const void*)k_multi3<P, true>));
+    for (int bpc : {4, 5, 6, 8}) {
+        const float t0 = run3<P, false>(a, b, ld, R, C, PR, M, pv, cus * bpc, reps);
+        const float t1 = run3<P, true>(a, b, ld, R, C, PR, M, pv, cus * bpc, reps);
+        printf("{\"size\": %d, \"P\": %d, \"bpc\": %d, \"v3_us\": %.1f, \"v3_pf_us\": %.1f, "
+               "\"vgpr\": %d, \"vgpr_pf\": %d}\n", R, P, bpc, t0 * 1e3, t1 * 1e3, fa0.numRegs,
+               fa1.numRegs);
+        fflush(stdout);
+    }
+}
+
+// Variant 4: one double per lane (64-double = 512-B chunks), U units in flight; halves the
+// pivot-row registers (P doubles per lane instead of 2P) so more waves fit per SIMD.
+template <int P>
+__device__ __forceinline__ double chain_exact1(double v, int row, int j, const Piv& pv,
+                                               const double* pr, const double* pc) {
+#pragma unroll
+    for (int l = 0; l < P; ++l) {
+        double num;
+        if (row == pv.r[l])
+            num = (j == pv.c[l]) ? 1.0 : -v;
+        else
+            num = (j == pv.c[l]) ? v : (v * pv.e[l] - pr[l] * pc[l]);
+        v = num / pv.e[l];
+    }
+    return v;
+}
+
+template <int P, int U>
+__global__ __launch_bounds__(kBlock) void k_multi4(const double* __restrict__ Tin,
+                                                    double* Tout, int64_t ld, int R, int C,
+                                                    const double* __restrict__ PR,
+                                                    const double* __restrict__ M, Piv pv) {
+    constexpr int kCh = kWave;
+    const int lane = threadIdx.x & 63;
+    const int NW = gridDim.x * kWaves;
+    const int w = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunks = (C + kCh - 1) / kCh;
+    const int64_t units = (int64_t)nchunks * R;
+    const int qs = NW / nchunks, rs = NW % nchunks;
+    int i = w / nchunks, ch = w % nchunks;
+    int ch_pr = -1;
+    bool cspecial = true;
+    double pr[P];
+    for (int64_t u = w; u < units; u += (int64_t)U * NW) {
+        int ii[U], cc[U];
+        double x[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            ii[k] = i;
+            cc[k] = ch;
+            ch += rs;
+            i += qs;
+            if (ch >= nchunks) {
+                ch -= nchunks;
+                ++i;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int j = cc[k] * kCh + lane;
+            x[k] = 0.0;
+            if (ii[k] < R && j < C) x[k] = __builtin_nontemporal_load(Tin + (int64_t)ii[k] * ld + j);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int row = ii[k];
+            if (row >= R) continue;
+            const int j = cc[k] * kCh + lane;
+            if (cc[k] != ch_pr) {
+                ch_pr = cc[k];
+                cspecial = false;
+                const int c0 = cc[k] * kCh;
+#pragma unroll
+                for (int l = 0; l < P; ++l) {
+                    pr[l] = (j < C) ? PR[(int64_t)l * ld + j] : 0.0;
+                    cspecial = cspecial || (pv.c[l] >= c0 && pv.c[l] < c0 + kCh);
+                }
+            }
+            double pc[P];
+            bool special = cspecial;
+#pragma unroll
+            for (int l = 0; l < P; ++l) {
+                pc[l] = M[(int64_t)row * kMaxP + l];
+                special = special || row == pv.r[l];
+            }
+            double v = x[k];
+            if (!special) {
+                double mn = kMaxAbs, mx = 0.0;
+#pragma unroll
+                for (int l = 0; l < P; ++l) {
+                    const double num = v * pv.e[l] - pr[l] * pc[l];
+                    mn = fmin(mn, fabs(num));
+                    mx = fmax(mx, fabs(num));
+                    const double t = num * pv.y[l];
+                    const double rr = fma(-pv.e[l], t, num);
+                    v = fma(rr, pv.y[l], t);
+                }
+                const bool in = mn >= kMinAbs && mx < kMaxAbs && v == v;
+                if (!__all(in)) v = chain_exact1<P>(x[k], row, j, pv, pr, pc);
+            } else {
+                v = chain_exact1<P>(v, row, j, pv, pr, pc);
+            }
+            if (j < C) __builtin_nontemporal_store(v, Tout + (int64_t)row * ld + j);
+        }
+    }
+}
+
+template <int P, int U>
+void row4(int R, const double* a, double* b, int64_t ld, int C, const double* PR, const double* M,
+          const Piv& pv, int cus, int reps) {
+    hipFuncAttributes fa;
+    CK(hipFuncGetAttributes(&fa, (const void*)k_multi4<P, U>));
+    for (int bpc : {5, 6, 8}) {
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        const int grid = cus * bpc;
+        hipLaunchKernelGGL((k_multi4<P, U>), dim3(grid), dim3(kBlock), 0, 0, a, b, ld, R, C, PR, M, pv);
+        CK(hipEventRecord(e0));
+        for (int t = 0; t < reps; ++t)
+            hipLaunchKernelGGL((k_multi4<P, U>), dim3(grid), dim3(kBlock), 0, 0, a, b, ld, R, C, PR,
+                               M, pv);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"size\": %d, \"P\": %d, \"U\": %d, \"bpc\": %d, \"v4_us\": %.1f, \"vgpr\": %d}\n",
+               R, P, U, bpc, ms / reps * 1e3, fa.numRegs);
+        fflush(stdout);
+    }
+}
+
 template <int P>
 float run2(const double* a, double* b, int64_t ld, int R, int C, const double* PR, const double* M,
            const Piv& pv, int grid, int reps) {
@@ -313,6 +572,21 @@ int main(int argc, char** argv) {
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int reps = N >= 16384 ? 10 : 40;
+    if (argc > 2 && argv[2][0] == '4') {
+        row4<4, 4>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        row4<6, 4>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        row4<8, 4>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        row4<8, 2>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        row4<8, 8>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        return 0;
+    }
+    if (argc > 2 && argv[2][0] == '3') {
+        row3<2>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        row3<4>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        row3<6>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        row3<8>(R, a, b, ld, C, PR, M, pv, cus, reps);
+        return 0;
+    }
     for (int bpc : {5, 8}) {
         const int grid = cus * bpc;
         char lab[64];
