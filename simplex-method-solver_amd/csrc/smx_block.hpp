@@ -690,7 +690,105 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
     }
 }
 
-template <int PMAX, bool NTL>
+// The sweep when every wave keeps one chunk for the whole pass (the grid's wave count is a
+// multiple of the chunks per row, update_grid's usual shape): the pivot-row slices are loaded
+// once, and the two units of a batch are computed together -- one "neither is special" branch,
+// their four element chains interleaved (ILP 4 instead of 2; tools/glds_probe.hip k_reg2:
+// 1120-1184 us vs 1176-1293 us at P = 8), one vote for both.  Same values as blk_sweep_body.
+template <int P, bool NTL>
+__device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* Tout, int64_t ld,
+                                                     int R, int C, const BlkHdr* __restrict__ h,
+                                                     const double* __restrict__ pr,
+                                                     const double* __restrict__ mul) {
+    const int lane = threadIdx.x & (kWave - 1);
+    int rq[P], cq[P];
+    double eq[P], yq[P];
+    bool allok = true;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        rq[q] = h->r[q];
+        cq[q] = h->c[q];
+        eq[q] = h->e[q];
+        yq[q] = h->y[q];
+        allok = allok && h->ok[q] != 0;
+    }
+    constexpr int kChunk = 2 * kWave;
+    const int NW = (int)gridDim.x * kUpdWaves;
+    const int w = (int)blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunks = (C + kChunk - 1) / kChunk;
+    const int qs = NW / nchunks;
+    const int ch = w % nchunks;
+    const int j = ch * kChunk + 2 * lane;
+    const int c0 = ch * kChunk;
+    dbl2 prs[P];
+    bool cspecial = !allok;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
+                         : dbl2{0.0, 0.0};
+        cspecial = cspecial || (cq[q] >= c0 && cq[q] < c0 + kChunk);
+    }
+    for (int i0 = w / nchunks; i0 < R; i0 += 2 * qs) {
+        const int i1 = i0 + qs;
+        const bool h1 = i1 < R;
+        dbl2 x0 = dbl2{0.0, 0.0}, x1 = dbl2{0.0, 0.0};
+        if (j < C) {
+            x0 = ld2<NTL>(Tin + (int64_t)i0 * ld + j);
+            if (h1) x1 = ld2<NTL>(Tin + (int64_t)i1 * ld + j);
+        }
+        const double* m0 = mul + (int64_t)i0 * kBlkMax;
+        const double* m1 = mul + (int64_t)(h1 ? i1 : i0) * kBlkMax;
+        double pc0[P], pc1[P];
+        bool special = cspecial || !h1;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            pc0[q] = m0[q];
+            pc1[q] = m1[q];
+            special = special || i0 == rq[q] || i1 == rq[q];
+        }
+        dbl2 v0 = x0, v1 = x1;
+        bool ok = false;
+        if (!special) {
+            double mn = kFdMaxAbs, mx = 0.0;
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const double e = eq[q], y = yq[q];
+                double n[4];
+                n[0] = v0[0] * e - prs[q][0] * pc0[q];
+                n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                n[2] = v1[0] * e - prs[q][0] * pc1[q];
+                n[3] = v1[1] * e - prs[q][1] * pc1[q];
+                double rr[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    mn = fmin(mn, fabs(n[k]));
+                    mx = fmax(mx, fabs(n[k]));
+                    const double t = n[k] * y;                // fd_div inside its window
+                    const double r = fma(-e, t, n[k]);
+                    rr[k] = fma(r, y, t);
+                }
+                v0 = dbl2{rr[0], rr[1]};
+                v1 = dbl2{rr[2], rr[3]};
+            }
+            // fmin/fmax skip NaN: a NaN numerator leaves a NaN result, caught by v == v
+            ok = __all(mn >= kFdMinAbs && mx < kFdMaxAbs && v0[0] == v0[0] && v0[1] == v0[1] &&
+                       v1[0] == v1[0] && v1[1] == v1[1]);
+        }
+        if (!ok) {
+            v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
+            if (h1) v1 = blk_exact<P>(x1, i1, j, rq, cq, eq, prs, pc1);
+        }
+        if (j < C) {
+            __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
+            if (h1)
+                __builtin_nontemporal_store(v1,
+                                            reinterpret_cast<dbl2*>(Tout + (int64_t)i1 * ld + j));
+        }
+    }
+}
+
+// FIXED: the launcher made the wave count a multiple of the chunks per row (blk_sweep_body_fixed)
+template <int PMAX, bool NTL, bool FIXED>
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b_other, int64_t ld,
                                                          int R, int C,
                                                          const BlkHdr* __restrict__ h,
@@ -702,7 +800,10 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
 #define SMX_BLK_CASE(n)                                                           \
     if constexpr (PMAX >= n) {                                                    \
         if (peff == n) {                                                          \
-            blk_sweep_body<n, NTL>(b_in, out, ld, R, C, h, pr, mul);              \
+            if constexpr (FIXED)                                                  \
+                blk_sweep_body_fixed<n, NTL>(b_in, out, ld, R, C, h, pr, mul);    \
+            else                                                                  \
+                blk_sweep_body<n, NTL>(b_in, out, ld, R, C, h, pr, mul);          \
             return;                                                               \
         }                                                                         \
     }

@@ -212,11 +212,12 @@ int num_cus() {
 
 // Grid = resident blocks, trimmed so the wave count is a multiple of the chunks per row (then
 // every wave keeps one pivot-row slice for the whole sweep).
-int update_grid(const smx_shape& s, const void* fn, int reserved) {
+int update_grid(const smx_shape& s, const void* fn, int reserved, int bpc = 0) {
     const int64_t R = s.rows + 1;
     const int64_t nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
     const int64_t units = nchunks * R;
-    int64_t blocks = (int64_t)num_cus() * blocks_per_cu(fn) - reserved;
+    if (bpc <= 0 || g_blocks_per_cu > 0) bpc = blocks_per_cu(fn);
+    int64_t blocks = (int64_t)num_cus() * bpc - reserved;
     if (blocks < 1) blocks = 1;
     // waves = a multiple of lcm(nchunks, waves per block) when that keeps >= 3/4 of them
     int64_t g = nchunks, h = kUpdWaves;
@@ -398,18 +399,23 @@ using BshPackFn = void (*)(const double*, int64_t, int, int, int, int, int, cons
                            const BlkHdr*, const smx_part*, int, const double*, const double*,
                            double*);
 
-template <bool NTL>
+template <bool NTL, bool FIXED>
 BlkSweepFn blk_sweep_fn_ntl(int P) {
     switch (P) {
-        case 1: return k_blk_sweep<1, NTL>;
-        case 2: return k_blk_sweep<2, NTL>;
-        case 3: return k_blk_sweep<3, NTL>;
-        case 4: return k_blk_sweep<4, NTL>;
-        case 5: return k_blk_sweep<5, NTL>;
-        case 6: return k_blk_sweep<6, NTL>;
-        case 7: return k_blk_sweep<7, NTL>;
-        default: return k_blk_sweep<8, NTL>;
+        case 1: return k_blk_sweep<1, NTL, FIXED>;
+        case 2: return k_blk_sweep<2, NTL, FIXED>;
+        case 3: return k_blk_sweep<3, NTL, FIXED>;
+        case 4: return k_blk_sweep<4, NTL, FIXED>;
+        case 5: return k_blk_sweep<5, NTL, FIXED>;
+        case 6: return k_blk_sweep<6, NTL, FIXED>;
+        case 7: return k_blk_sweep<7, NTL, FIXED>;
+        default: return k_blk_sweep<8, NTL, FIXED>;
     }
+}
+
+BlkSweepFn blk_sweep_fn(int P, bool ntl, bool fixed) {
+    if (ntl) return fixed ? blk_sweep_fn_ntl<true, true>(P) : blk_sweep_fn_ntl<true, false>(P);
+    return fixed ? blk_sweep_fn_ntl<false, true>(P) : blk_sweep_fn_ntl<false, false>(P);
 }
 
 template <bool SH>
@@ -494,8 +500,17 @@ int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, con
 int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, char* blk,
                        const BlkLayout& L, hipStream_t st) {
     const bool ntl = (int64_t)(s.rows + 1) * s.ld * 8 > kCacheTable;
-    BlkSweepFn fn = ntl ? blk_sweep_fn_ntl<true>(P) : blk_sweep_fn_ntl<false>(P);
-    const int grid = update_grid(s, (const void*)fn, 0);
+    // the fixed-chunk form when the grid's wave count is a multiple of the chunks per row
+    const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
+    // 8 blocks per CU for the widest blocks (fixed form at 62 VGPRs: 8 waves per SIMD fit;
+    // 16384^2, P = 8: 1294 us per sweep vs 1438 at 5 and 1351 at 6, tools/block_bench.py --bpc)
+    const int bpc = P >= 7 ? 8 : 0;
+    BlkSweepFn fn = blk_sweep_fn(P, ntl, true);
+    int grid = update_grid(s, (const void*)fn, 0, bpc);
+    if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
+        fn = blk_sweep_fn(P, ntl, false);
+        grid = update_grid(s, (const void*)fn, 0);
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, tin, tother, s.ld, s.rows + 1,
                        s.m + 1, reinterpret_cast<const BlkHdr*>(blk),
                        reinterpret_cast<const double*>(blk + L.mul),

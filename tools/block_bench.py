@@ -24,12 +24,15 @@ def main() -> None:
     ap.add_argument("--sizes", default="4096,8192,16384")
     ap.add_argument("--pivots", default="1,2,3,4,5,6,8")
     ap.add_argument("--k", type=int, default=48)
+    ap.add_argument("--bpc", type=int, default=0, help="blocks per CU of the sweep (0: library)")
     a = ap.parse_args()
     import numpy as np
     import torch
     from simplex_mi355x import _lib, lp
     from simplex_mi355x.device import DeviceTableau
     _lib.tune_resident(-1)
+    if a.bpc:
+        _lib.check(_lib.load().smx_tune_set(-2, a.bpc), "smx_tune_set")
     for N in (int(x) for x in a.sizes.split(",")):
         n = m = N - 1
         T = lp.dense_tableau("uniform", 0, n, m)
@@ -55,7 +58,7 @@ def main() -> None:
             ctl = dev.sync_state()
             log = dev.read_log(0, int(ctl["npivots"]))
             tab = dev.download().view(np.int64)
-            row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "k": k,
+            row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "k": k, "bpc": a.bpc,
                    "us_per_pivot": ms * 1e3 / k, "pivots_s": k / ms * 1e3,
                    "npivots": int(ctl["npivots"])}
             if P == 0:

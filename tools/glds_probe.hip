@@ -243,6 +243,88 @@ __global__ __launch_bounds__(kBlock) void k_reg(const double* __restrict__ Tin, 
     }
 }
 
+// U = 2 units computed together: one branch for "neither is special", their four element chains
+// interleaved in one unrolled loop (ILP 4 per wave instead of 2), one vote for both
+template <int P>
+__global__ __launch_bounds__(kBlock) void k_reg2(const double* __restrict__ Tin, double* Tout,
+                                                  int64_t ld, int R, int C,
+                                                  const double* __restrict__ PR,
+                                                  const double* __restrict__ M, Piv pv) {
+    const int lane = threadIdx.x & 63;
+    const int NW = gridDim.x * kWaves;
+    const int w = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunks = (C + kChunk - 1) / kChunk;
+    const int64_t units = (int64_t)nchunks * R;
+    const int qs = NW / nchunks;
+    // fixed chunk per wave (NW a multiple of nchunks)
+    const int ch = w % nchunks;
+    const int j = ch * kChunk + 2 * lane;
+    dbl2 pr[P];
+    bool cspecial = false;
+#pragma unroll
+    for (int l = 0; l < P; ++l) {
+        pr[l] = (j < C) ? *reinterpret_cast<const dbl2*>(PR + (int64_t)l * ld + j) : dbl2{0.0, 0.0};
+        cspecial = cspecial || (pv.c[l] >= ch * kChunk && pv.c[l] < ch * kChunk + kChunk);
+    }
+    int i = w / nchunks;
+    for (int64_t u = w; u < units; u += 2 * (int64_t)NW) {
+        const int i0 = i, i1 = i + qs;
+        i += 2 * qs;
+        const bool h1 = i1 < R;
+        dbl2 x0 = dbl2{0.0, 0.0}, x1 = dbl2{0.0, 0.0};
+        if (j < C) {
+            x0 = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(Tin + (int64_t)i0 * ld + j));
+            if (h1)
+                x1 = __builtin_nontemporal_load(
+                    reinterpret_cast<const dbl2*>(Tin + (int64_t)i1 * ld + j));
+        }
+        double pc0[P], pc1[P];
+        bool special = cspecial || !h1;
+#pragma unroll
+        for (int l = 0; l < P; ++l) {
+            pc0[l] = M[(int64_t)i0 * kMaxP + l];
+            pc1[l] = h1 ? M[(int64_t)i1 * kMaxP + l] : 0.0;
+            special = special || i0 == pv.r[l] || i1 == pv.r[l];
+        }
+        dbl2 v0 = x0, v1 = x1;
+        bool ok = false;
+        if (!special) {
+            double mn = kMaxAbs, mx = 0.0;
+#pragma unroll
+            for (int l = 0; l < P; ++l) {
+                const double e = pv.e[l], y = pv.y[l];
+                double n[4];
+                n[0] = v0[0] * e - pr[l][0] * pc0[l];
+                n[1] = v0[1] * e - pr[l][1] * pc0[l];
+                n[2] = v1[0] * e - pr[l][0] * pc1[l];
+                n[3] = v1[1] * e - pr[l][1] * pc1[l];
+                double r[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    mn = fmin(mn, fabs(n[q]));
+                    mx = fmax(mx, fabs(n[q]));
+                    const double t = n[q] * y;
+                    const double rr = fma(-e, t, n[q]);
+                    r[q] = fma(rr, y, t);
+                }
+                v0 = dbl2{r[0], r[1]};
+                v1 = dbl2{r[2], r[3]};
+            }
+            ok = __all(mn >= kMinAbs && mx < kMaxAbs && v0[0] == v0[0] && v0[1] == v0[1] &&
+                       v1[0] == v1[0] && v1[1] == v1[1]);
+        }
+        if (!ok) {
+            v0 = steps_exact<P>(x0, i0, j, pv, pr, pc0);
+            if (h1) v1 = steps_exact<P>(x1, i1, j, pv, pr, pc1);
+        }
+        if (j < C) {
+            __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
+            if (h1)
+                __builtin_nontemporal_store(v1, reinterpret_cast<dbl2*>(Tout + (int64_t)i1 * ld + j));
+        }
+    }
+}
+
 __global__ void k_fill(double* a, int64_t n, unsigned long long seed) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -328,7 +410,27 @@ int main(int argc, char** argv) {
         free(h1);
         free(h2);
     }
+    hipLaunchKernelGGL((k_reg2<8>), dim3(cus * 5), dim3(kBlock), 0, 0, a, b, ld, R, C, PR, M, pv);
+    CK(hipDeviceSynchronize());
+    {
+        const size_t nb = (size_t)R * ld * 8;
+        double* h1 = (double*)malloc(nb);
+        double* h2 = (double*)malloc(nb);
+        CK(hipMemcpy(h1, chk, nb, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h2, b, nb, hipMemcpyDeviceToHost));
+        long bad = 0;
+        for (long q = 0; q < (long)R * ld; ++q)
+            if (__builtin_memcmp(&h1[q], &h2[q], 8) != 0) ++bad;
+        printf("{\"check\": \"reg2 vs reg\", \"mismatches\": %ld}\n", bad);
+        fflush(stdout);
+        free(h1);
+        free(h2);
+    }
     row("reg", 8, k_reg<8>, cus, a, b, ld, R, C, PR, M, pv, reps);
+    row("reg2", 8, k_reg2<8>, cus, a, b, ld, R, C, PR, M, pv, reps);
+    row("reg2", 6, k_reg2<6>, cus, a, b, ld, R, C, PR, M, pv, reps);
+    row("reg2", 4, k_reg2<4>, cus, a, b, ld, R, C, PR, M, pv, reps);
+    return 0;
     row("glds_s3", 8, k_glds<8, 3, 0>, cus, a, b, ld, R, C, PR, M, pv, reps);
     row("glds_s4", 8, k_glds<8, 4, 0>, cus, a, b, ld, R, C, PR, M, pv, reps);
     row("glds_s3_nt", 8, k_glds<8, 3, 2>, cus, a, b, ld, R, C, PR, M, pv, reps);
