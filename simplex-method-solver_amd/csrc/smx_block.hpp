@@ -695,7 +695,33 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
 // once, and the two units of a batch are computed together -- one "neither is special" branch,
 // their four element chains interleaved (ILP 4 instead of 2; tools/glds_probe.hip k_reg2:
 // 1120-1184 us vs 1176-1293 us at P = 8), one vote for both.  Same values as blk_sweep_body.
-template <int P, bool NTL>
+// Batch index (rows base + t*qs, batch t >> 1) of pivot q's row on this wave, lane q of the
+// wave holding it (0x7fffffff: another wave's row, or no pivot q)
+template <int P>
+__device__ __forceinline__ int blk_special_batch(const BlkHdr* __restrict__ h, int base, int qs) {
+    const int q = threadIdx.x & (kWave - 1);
+    int tb = 0x7fffffff;
+    if (q < P) {
+        const int rq = h->r[q];
+        const int d = rq - base;
+        if (rq >= 0 && d >= 0 && d % qs == 0) tb = (d / qs) >> 1;
+    }
+    return tb;
+}
+
+// smallest batch index > t among lanes 0..P-1 of tb (wave-uniform)
+template <int P>
+__device__ __forceinline__ int blk_next_batch(int tb, int t) {
+    int best = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        const int v = __builtin_amdgcn_readlane(tb, q);
+        best = (v > t && v < best) ? v : best;
+    }
+    return best;
+}
+
+template <int P, bool NTL, bool PF>
 __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* Tout, int64_t ld,
                                                      int R, int C, const BlkHdr* __restrict__ h,
                                                      const double* __restrict__ pr,
@@ -728,23 +754,22 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
                          : dbl2{0.0, 0.0};
         cspecial = cspecial || (cq[q] >= c0 && cq[q] < c0 + kChunk);
     }
-    for (int i0 = w / nchunks; i0 < R; i0 += 2 * qs) {
+    const int base = w / nchunks;
+    const int tbq = blk_special_batch<P>(h, base, qs);
+    int tsp = blk_next_batch<P>(tbq, -1);
+    // one batch: rows i0 and i1 = i0 + qs (batch t), their loads x0 / x1 already issued
+    auto batch = [&](dbl2 x0, dbl2 x1, int i0, int t) {
         const int i1 = i0 + qs;
         const bool h1 = i1 < R;
-        dbl2 x0 = dbl2{0.0, 0.0}, x1 = dbl2{0.0, 0.0};
-        if (j < C) {
-            x0 = ld2<NTL>(Tin + (int64_t)i0 * ld + j);
-            if (h1) x1 = ld2<NTL>(Tin + (int64_t)i1 * ld + j);
-        }
         const double* m0 = mul + (int64_t)i0 * kBlkMax;
         const double* m1 = mul + (int64_t)(h1 ? i1 : i0) * kBlkMax;
         double pc0[P], pc1[P];
-        bool special = cspecial || !h1;
+        const bool special = cspecial || !h1 || t == tsp;
+        if (t == tsp) tsp = blk_next_batch<P>(tbq, t);
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             pc0[q] = m0[q];
             pc1[q] = m1[q];
-            special = special || i0 == rq[q] || i1 == rq[q];
         }
         dbl2 v0 = x0, v1 = x1;
         bool ok = false;
@@ -763,9 +788,9 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
                 for (int k = 0; k < 4; ++k) {
                     mn = fmin(mn, fabs(n[k]));
                     mx = fmax(mx, fabs(n[k]));
-                    const double t = n[k] * y;                // fd_div inside its window
-                    const double r = fma(-e, t, n[k]);
-                    rr[k] = fma(r, y, t);
+                    const double tq = n[k] * y;               // fd_div inside its window
+                    const double r = fma(-e, tq, n[k]);
+                    rr[k] = fma(r, y, tq);
                 }
                 v0 = dbl2{rr[0], rr[1]};
                 v1 = dbl2{rr[2], rr[3]};
@@ -775,6 +800,13 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
                        v1[0] == v1[0] && v1[1] == v1[1]);
         }
         if (!ok) {
+            if (PF) {
+                // reloaded (this batch's elements are not written yet, even in place), so the
+                // inputs need not stay live beside the chains
+                const int jl = min(j, (C - 1) & ~1);
+                x0 = *reinterpret_cast<const dbl2*>(Tin + (int64_t)i0 * ld + jl);
+                if (h1) x1 = *reinterpret_cast<const dbl2*>(Tin + (int64_t)i1 * ld + jl);
+            }
             v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
             if (h1) v1 = blk_exact<P>(x1, i1, j, rq, cq, eq, prs, pc1);
         }
@@ -784,11 +816,58 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
                 __builtin_nontemporal_store(v1,
                                             reinterpret_cast<dbl2*>(Tout + (int64_t)i1 * ld + j));
         }
+    };
+    if (!PF) {
+        int t = 0;
+        for (int i0 = base; i0 < R; i0 += 2 * qs, ++t) {
+            const int i1 = i0 + qs;
+            dbl2 x0 = dbl2{0.0, 0.0}, x1 = dbl2{0.0, 0.0};
+            if (j < C) {
+                x0 = ld2<NTL>(Tin + (int64_t)i0 * ld + j);
+                if (i1 < R) x1 = ld2<NTL>(Tin + (int64_t)i1 * ld + j);
+            }
+            batch(x0, x1, i0, t);
+        }
+        return;
     }
+    // PF: the next batch's two loads are issued before this batch's arithmetic, into the other of
+    // two register sets, without branches (row and column clamped into the table; a clamped row's
+    // or lane's values are never stored).  The loads are inline asm with explicit waits: the
+    // compiler's own vmcnt tracking waits for them at the loop edge.  In-order vmcnt (gfx9): before
+    // a set is used, the ops issued after its loads are the previous batch's stores (two, as every
+    // wave holds a lane j < C and only the last batch has no row i1) and the other set's loads.
+    const int jc = min(j, (C - 1) & ~1);
+    auto ldc = [&](int row) {
+        dbl2 v;
+        const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
+        if (NTL)
+            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+        else
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+        return v;
+    };
+    dbl2 a0 = ldc(base), a1 = ldc(base + qs);
+    dbl2 b0 = ldc(base + 2 * qs), b1 = ldc(base + 3 * qs);
+    asm volatile("s_waitcnt vmcnt(2)" : "+v"(a0), "+v"(a1) :: "memory");
+    int t = 0;
+    for (int i0 = base; i0 < R; i0 += 4 * qs, t += 2) {
+        batch(a0, a1, i0, t);
+        if (i0 + 2 * qs >= R) break;
+        a0 = ldc(i0 + 4 * qs);
+        a1 = ldc(i0 + 5 * qs);
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(b0), "+v"(b1) :: "memory");
+        batch(b0, b1, i0 + 2 * qs, t + 1);
+        if (i0 + 4 * qs >= R) break;
+        b0 = ldc(i0 + 6 * qs);
+        b1 = ldc(i0 + 7 * qs);
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(a0), "+v"(a1) :: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no load in flight at exit
 }
 
-// FIXED: the launcher made the wave count a multiple of the chunks per row (blk_sweep_body_fixed)
-template <int PMAX, bool NTL, bool FIXED>
+// FORM 0: generic; 1: the launcher made the wave count a multiple of the chunks per row
+// (blk_sweep_body_fixed); 2: that, with the next batch's loads issued before this batch's arithmetic
+template <int PMAX, bool NTL, int FORM>
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b_other, int64_t ld,
                                                          int R, int C,
                                                          const BlkHdr* __restrict__ h,
@@ -800,8 +879,8 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
 #define SMX_BLK_CASE(n)                                                           \
     if constexpr (PMAX >= n) {                                                    \
         if (peff == n) {                                                          \
-            if constexpr (FIXED)                                                  \
-                blk_sweep_body_fixed<n, NTL>(b_in, out, ld, R, C, h, pr, mul);    \
+            if constexpr (FORM > 0)                                               \
+                blk_sweep_body_fixed<n, NTL, FORM == 2>(b_in, out, ld, R, C, h, pr, mul); \
             else                                                                  \
                 blk_sweep_body<n, NTL>(b_in, out, ld, R, C, h, pr, mul);          \
             return;                                                               \

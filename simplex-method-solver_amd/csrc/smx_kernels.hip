@@ -399,23 +399,27 @@ using BshPackFn = void (*)(const double*, int64_t, int, int, int, int, int, cons
                            const BlkHdr*, const smx_part*, int, const double*, const double*,
                            double*);
 
-template <bool NTL, bool FIXED>
+template <bool NTL, int FORM>
 BlkSweepFn blk_sweep_fn_ntl(int P) {
     switch (P) {
-        case 1: return k_blk_sweep<1, NTL, FIXED>;
-        case 2: return k_blk_sweep<2, NTL, FIXED>;
-        case 3: return k_blk_sweep<3, NTL, FIXED>;
-        case 4: return k_blk_sweep<4, NTL, FIXED>;
-        case 5: return k_blk_sweep<5, NTL, FIXED>;
-        case 6: return k_blk_sweep<6, NTL, FIXED>;
-        case 7: return k_blk_sweep<7, NTL, FIXED>;
-        default: return k_blk_sweep<8, NTL, FIXED>;
+        case 1: return k_blk_sweep<1, NTL, FORM>;
+        case 2: return k_blk_sweep<2, NTL, FORM>;
+        case 3: return k_blk_sweep<3, NTL, FORM>;
+        case 4: return k_blk_sweep<4, NTL, FORM>;
+        case 5: return k_blk_sweep<5, NTL, FORM>;
+        case 6: return k_blk_sweep<6, NTL, FORM>;
+        case 7: return k_blk_sweep<7, NTL, FORM>;
+        default: return k_blk_sweep<8, NTL, FORM>;
     }
 }
 
-BlkSweepFn blk_sweep_fn(int P, bool ntl, bool fixed) {
-    if (ntl) return fixed ? blk_sweep_fn_ntl<true, true>(P) : blk_sweep_fn_ntl<true, false>(P);
-    return fixed ? blk_sweep_fn_ntl<false, true>(P) : blk_sweep_fn_ntl<false, false>(P);
+BlkSweepFn blk_sweep_fn(int P, bool ntl, int form) {
+    if (ntl) {
+        if (form == 2) return blk_sweep_fn_ntl<true, 2>(P);
+        return form ? blk_sweep_fn_ntl<true, 1>(P) : blk_sweep_fn_ntl<true, 0>(P);
+    }
+    if (form == 2) return blk_sweep_fn_ntl<false, 2>(P);
+    return form ? blk_sweep_fn_ntl<false, 1>(P) : blk_sweep_fn_ntl<false, 0>(P);
 }
 
 template <bool SH>
@@ -502,13 +506,21 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     const bool ntl = (int64_t)(s.rows + 1) * s.ld * 8 > kCacheTable;
     // the fixed-chunk form when the grid's wave count is a multiple of the chunks per row
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    // 8 blocks per CU for the widest blocks (fixed form at 62 VGPRs: 8 waves per SIMD fit;
-    // 16384^2, P = 8: 1294 us per sweep vs 1438 at 5 and 1351 at 6, tools/block_bench.py --bpc)
-    const int bpc = P >= 7 ? 8 : 0;
-    BlkSweepFn fn = blk_sweep_fn(P, ntl, true);
+    // P >= 7: the prefetching fixed form (74 VGPRs) at 7 blocks per CU -- 16384^2: 1094-1105 us
+    // per sweep at P = 8 vs 1139-1144 for the plain fixed form at 8 blocks per CU, 981 vs
+    // 1057-1071 at P = 7 (same box, tools/block_bench.py, profiles/r01_block_sweep_pf.jsonl);
+    // P <= 6: the plain fixed form.  SMX_BLK_PF (experiments): 0 = never prefetch, N >= 2 =
+    // always, at N blocks per CU.
+    static const int pf_env = [] {
+        const char* e = getenv("SMX_BLK_PF");
+        return e ? atoi(e) : -1;
+    }();
+    const bool pf = pf_env < 0 ? P >= 7 : pf_env >= 2;
+    const int bpc = pf ? (pf_env >= 2 ? pf_env : 7) : 0;
+    BlkSweepFn fn = blk_sweep_fn(P, ntl, pf ? 2 : 1);
     int grid = update_grid(s, (const void*)fn, 0, bpc);
     if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
-        fn = blk_sweep_fn(P, ntl, false);
+        fn = blk_sweep_fn(P, ntl, 0);
         grid = update_grid(s, (const void*)fn, 0);
     }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, tin, tother, s.ld, s.rows + 1,
