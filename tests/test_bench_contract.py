@@ -1,0 +1,79 @@
+"""The committed bench evidence keeps the driver's contract (CPU only: reads profiles/).
+
+profiles/r01_bench_default.json is the default `python bench.py` line of this round's GPU run;
+profiles/r01_block_16384_* are the rocprofv3 kernel-trace stats and PMC passes of the same
+command (tools/profile_round.sh).  The checks: the JSON line's keys and types, the roofline
+arithmetic (achieved = algorithmic bytes / average launch, frac = achieved / peak), the
+cpu_baseline block, and that the HIP-event launch average agrees with rocprofv3's.
+"""
+import csv
+import json
+import os
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(REPO, "profiles")
+
+
+def _line(name):
+    with open(os.path.join(PROF, name)) as fh:
+        lines = [ln for ln in fh.read().splitlines() if ln.startswith("{")]
+    assert lines, name
+    return json.loads(lines[-1])
+
+
+def _rocprof_avg_ms(name, needle):
+    with open(os.path.join(PROF, name)) as fh:
+        rows = [r for r in csv.DictReader(fh) if needle in r["Name"]]
+    assert rows, needle
+    calls = sum(int(r["Calls"]) for r in rows)
+    total = sum(float(r["TotalDurationNs"]) for r in rows)
+    return total / calls * 1e-6
+
+
+def test_default_line_keys():
+    rec = _line("r01_bench_default.json")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in rec, k
+    assert rec["unit"] == "pivots/s" and rec["dtype"] == "f64" and rec["n_gpus"] == 1
+    assert rec["higher_is_better"] is True and rec["vs_baseline"] is None
+    assert "workload" in rec["config"] and rec["config"]["rows"] == 16384
+    assert rec["trajectory_valid"] is True
+    assert rec["value"] == pytest.approx(1e3 / rec["ms_per_step"], rel=1e-6)
+
+
+def test_roofline_arithmetic():
+    r = _line("r01_bench_default.json")["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    ach = r["algorithmic_bytes_per_launch"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
+    assert r["achieved"] == pytest.approx(ach, rel=1e-9)
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-9)
+    assert r["algorithmic_bytes_per_launch"] == 16.0 * 16384 * 16384
+    # PMC traffic within a few percent of the algorithmic bytes (no re-reads)
+    assert r["traffic"] is not None
+    assert 1.0 <= r["traffic"] / r["algorithmic_bytes_per_launch"] < 1.03
+
+
+def test_cpu_baseline_block():
+    cb = _line("r01_bench_default.json")["cpu_baseline"]
+    assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1
+    assert cb["value"] > 0 and cb["unit"] == "pivots/s" and cb["sample"]
+
+
+def test_event_average_agrees_with_rocprof():
+    rec = _line("r01_block_16384_bench.log")
+    r = rec["roofline"]
+    prof = _rocprof_avg_ms("r01_block_16384_kernel_stats.csv", "k_blk_sweep<8")
+    assert r["kernel"] == "k_blk_sweep<8>"
+    assert abs(r["avg_kernel_ms"] - prof) / prof < 0.10, (r["avg_kernel_ms"], prof)
+
+
+def test_pmc_summary_matches_csv_passes():
+    with open(os.path.join(PROF, "pmc_traffic.json")) as fh:
+        t = json.load(fh)["16384x16384/k_blk_sweep<8>"]
+    assert t["bytes_per_launch"] == pytest.approx(t["read_bytes_corrected"] + t["write_bytes"])
+    assert t["read_bytes_corrected"] == pytest.approx(2 * 1024 * t["fetch_size_kib_median"])
+    assert t["write_bytes"] == pytest.approx(1024 * t["write_size_kib_median"])
