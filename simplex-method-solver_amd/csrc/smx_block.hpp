@@ -7,6 +7,11 @@
 
 namespace {
 
+template <bool B>
+struct SmxBool {
+    static constexpr bool value = B;
+};
+
 // ---------------------------------------------------------------------------------------------
 // Why: one pivot reads and writes every element once (16 B), so a chain of single-pivot sweeps is
 // pinned at the copy rate of HBM (16384^2: ~815 us per pivot, 95 % of the measured copy ceiling).
@@ -566,6 +571,19 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
 // the result against NaN) and otherwise the unit is recomputed with the hardware division.
 constexpr double kFdMinAbs = 0x1p-127;   // biased exponent 896
 constexpr double kFdMaxAbs = 0x1p130;    // biased exponent 1152 is the last inside
+// The same window on the high dword with 32-bit integer ops: t = (hi << 1) + kWinBias (mod 2^32)
+// drops the sign and is < kWinSpan exactly when the biased exponent lies in [896, 1152] (fd_in);
+// NaN, infinities, zeros and denormals fall outside.  A running unsigned max per lane replaces
+// the two fp64 min/max per element and pivot (tools/sweep_probe.hip, profiles/r02_sweep_probe*).
+constexpr uint32_t kWinBias = 0x90000000u;   // -(896 << 21) mod 2^32
+constexpr uint32_t kWinSpan = 0x20200000u;   // (1153 - 896) << 21
+__device__ __forceinline__ uint32_t win_term(double n) {
+    uint32_t t;
+    // one v_lshl_add_u32 (written out: the compiler turns the shift of the high dword into an
+    // alignbit + and + add sequence)
+    asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(t) : "v"(__double2hiint(n)), "s"(kWinBias));
+    return t;
+}
 
 template <int P>
 __device__ __forceinline__ dbl2 blk_exact(dbl2 v, int row, int j, const int* rq, const int* cq,
@@ -615,7 +633,7 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
     const int qs = NW / nchunks, rs = NW % nchunks;
     int i = w / nchunks, ch = w % nchunks;
     int ch_pr = -1;
-    bool chunk_special = true;
+    uint32_t cbits = 0;   // bit 2q+hh: column j+hh of this chunk is pivot q's column
     dbl2 prs[P];
     for (int64_t u = w; u < units; u += (int64_t)U * NW) {
         int ii[U], cc[U];
@@ -644,18 +662,18 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
             const int j = cc[k] * kChunk + 2 * lane;
             if (cc[k] != ch_pr) {
                 ch_pr = cc[k];
-                chunk_special = !allok;
-                const int c0 = cc[k] * kChunk;
+                cbits = 0;
 #pragma unroll
                 for (int q = 0; q < P; ++q) {
                     prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
                                      : dbl2{0.0, 0.0};
-                    chunk_special = chunk_special || (cq[q] >= c0 && cq[q] < c0 + kChunk);
+                    cbits |= (cq[q] == j ? 1u : 0u) << (2 * q);
+                    cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
                 }
             }
             const double* mr = mul + (int64_t)row * kBlkMax;
             double pc[P];
-            bool special = chunk_special;
+            bool special = !allok;
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 pc[q] = mr[q];
@@ -663,24 +681,22 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
             }
             dbl2 v = x[k];
             if (!special) {
-                double mn = kFdMaxAbs, mx = 0.0;
+                uint32_t wt = 0;
 #pragma unroll
                 for (int q = 0; q < P; ++q) {
 #pragma unroll
                     for (int hh = 0; hh < 2; ++hh) {
                         const double a = v[hh] * eq[q];
                         const double b = prs[q][hh] * pc[q];
-                        const double num = a - b;
-                        mn = fmin(mn, fabs(num));
-                        mx = fmax(mx, fabs(num));
+                        // the pivot column's numerator is the element itself (simplex.py:159-160)
+                        const double num = ((cbits >> (2 * q + hh)) & 1u) ? v[hh] : a - b;
+                        wt = max(wt, win_term(num));
                         const double t = num * yq[q];          // fd_div inside its window
                         const double rr = fma(-eq[q], t, num);
                         v[hh] = fma(rr, yq[q], t);
                     }
                 }
-                // fmin/fmax skip NaN: a NaN numerator leaves a NaN result, caught by v == v
-                const bool in = mn >= kFdMinAbs && mx < kFdMaxAbs && v[0] == v[0] && v[1] == v[1];
-                if (!__all(in)) v = blk_exact<P>(x[k], row, j, rq, cq, eq, prs, pc);
+                if (!__all(wt < kWinSpan)) v = blk_exact<P>(x[k], row, j, rq, cq, eq, prs, pc);
             } else {
                 v = blk_exact<P>(v, row, j, rq, cq, eq, prs, pc);
             }
@@ -747,13 +763,21 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
     const int j = ch * kChunk + 2 * lane;
     const int c0 = ch * kChunk;
     dbl2 prs[P];
-    bool cspecial = !allok;
+    // a chunk holding a pivot column takes the fast path with the column's numerator selected
+    // (the element itself, simplex.py:159-160) instead of the exact path for all its rows: those
+    // waves were the sweep's stragglers (1.10-1.16 ms -> 0.83-0.90 ms per 8-pivot sweep at
+    // 16384^2, tools/sweep_probe.hip)
+    bool colchunk = false;
+    uint32_t cbits = 0;   // bit 2q+hh: column j+hh is pivot q's column
 #pragma unroll
     for (int q = 0; q < P; ++q) {
         prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
                          : dbl2{0.0, 0.0};
-        cspecial = cspecial || (cq[q] >= c0 && cq[q] < c0 + kChunk);
+        colchunk = colchunk || (cq[q] >= c0 && cq[q] < c0 + kChunk);
+        cbits |= (cq[q] == j ? 1u : 0u) << (2 * q);
+        cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
     }
+    const bool cspecial = !allok;
     const int base = w / nchunks;
     const int tbq = blk_special_batch<P>(h, base, qs);
     int tsp = blk_next_batch<P>(tbq, -1);
@@ -773,8 +797,10 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
         }
         dbl2 v0 = x0, v1 = x1;
         bool ok = false;
-        if (!special) {
-            double mn = kFdMaxAbs, mx = 0.0;
+        // the fast path: numerators in the window form, one integer window term per element
+        auto fast = [&](auto selc) {
+            constexpr bool SEL = decltype(selc)::value;
+            uint32_t wt = 0;
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 const double e = eq[q], y = yq[q];
@@ -783,11 +809,17 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
                 n[1] = v0[1] * e - prs[q][1] * pc0[q];
                 n[2] = v1[0] * e - prs[q][0] * pc1[q];
                 n[3] = v1[1] * e - prs[q][1] * pc1[q];
+                if (SEL) {
+                    const bool s0 = (cbits >> (2 * q)) & 1u, s1 = (cbits >> (2 * q + 1)) & 1u;
+                    n[0] = s0 ? v0[0] : n[0];
+                    n[1] = s1 ? v0[1] : n[1];
+                    n[2] = s0 ? v1[0] : n[2];
+                    n[3] = s1 ? v1[1] : n[3];
+                }
                 double rr[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    mn = fmin(mn, fabs(n[k]));
-                    mx = fmax(mx, fabs(n[k]));
+                    wt = max(wt, win_term(n[k]));
                     const double tq = n[k] * y;               // fd_div inside its window
                     const double r = fma(-e, tq, n[k]);
                     rr[k] = fma(r, y, tq);
@@ -795,9 +827,13 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
                 v0 = dbl2{rr[0], rr[1]};
                 v1 = dbl2{rr[2], rr[3]};
             }
-            // fmin/fmax skip NaN: a NaN numerator leaves a NaN result, caught by v == v
-            ok = __all(mn >= kFdMinAbs && mx < kFdMaxAbs && v0[0] == v0[0] && v0[1] == v0[1] &&
-                       v1[0] == v1[0] && v1[1] == v1[1]);
+            ok = __all(wt < kWinSpan);   // NaN / inf / zero numerators fall outside the window
+        };
+        if (!special) {
+            if (colchunk)
+                fast(SmxBool<true>{});
+            else
+                fast(SmxBool<false>{});
         }
         if (!ok) {
             if (PF) {
@@ -865,26 +901,43 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no load in flight at exit
 }
 
-// FORM 0: generic; 1: the launcher made the wave count a multiple of the chunks per row
-// (blk_sweep_body_fixed); 2: that, with the next batch's loads issued before this batch's arithmetic
-template <int PMAX, bool NTL, int FORM>
+// The sweep of a block that applied all P of its pivots (h->peff == P; otherwise it does nothing
+// and k_blk_sweep_part handles the block): one body per kernel, so the register allocation is
+// that body's alone.  FORM 0: generic; 1: the launcher made the wave count a multiple of the
+// chunks per row (blk_sweep_body_fixed); 2: that, with the next batch's loads issued before this
+// batch's arithmetic.  In place when P is even, so the table after d pivots is in
+// buf[(parity + d) & 1].
+template <int P, bool NTL, int FORM>
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b_other, int64_t ld,
                                                          int R, int C,
                                                          const BlkHdr* __restrict__ h,
                                                          const double* __restrict__ mul,
                                                          const double* __restrict__ pr) {
+    if (h->peff != P) return;
+    double* out = (P & 1) ? b_other : b_in;
+    if constexpr (FORM > 0)
+        blk_sweep_body_fixed<P, NTL, FORM == 2>(b_in, out, ld, R, C, h, pr, mul);
+    else
+        blk_sweep_body<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
+}
+
+// A block that stopped early (a terminal outcome after peff < P pivots, peff > 0): the generic
+// body for its count; launched after k_blk_sweep<P>, it does nothing when peff is 0 or P.
+template <int PMAX, bool NTL>
+__global__ __launch_bounds__(kUpdBlock) void k_blk_sweep_part(double* b_in, double* b_other,
+                                                              int64_t ld, int R, int C,
+                                                              const BlkHdr* __restrict__ h,
+                                                              const double* __restrict__ mul,
+                                                              const double* __restrict__ pr) {
     const int peff = h->peff;
-    if (peff <= 0) return;
+    if (peff <= 0 || peff >= PMAX) return;
     double* out = (peff & 1) ? b_other : b_in;
-#define SMX_BLK_CASE(n)                                                           \
-    if constexpr (PMAX >= n) {                                                    \
-        if (peff == n) {                                                          \
-            if constexpr (FORM > 0)                                               \
-                blk_sweep_body_fixed<n, NTL, FORM == 2>(b_in, out, ld, R, C, h, pr, mul); \
-            else                                                                  \
-                blk_sweep_body<n, NTL>(b_in, out, ld, R, C, h, pr, mul);          \
-            return;                                                               \
-        }                                                                         \
+#define SMX_BLK_CASE(n)                                                    \
+    if constexpr (PMAX > n) {                                              \
+        if (peff == n) {                                                   \
+            blk_sweep_body<n, NTL>(b_in, out, ld, R, C, h, pr, mul);       \
+            return;                                                        \
+        }                                                                  \
     }
     SMX_BLK_CASE(1)
     SMX_BLK_CASE(2)
@@ -893,7 +946,6 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
     SMX_BLK_CASE(5)
     SMX_BLK_CASE(6)
     SMX_BLK_CASE(7)
-    SMX_BLK_CASE(8)
 #undef SMX_BLK_CASE
 }
 

@@ -422,6 +422,19 @@ BlkSweepFn blk_sweep_fn(int P, bool ntl, int form) {
     return form ? blk_sweep_fn_ntl<false, 1>(P) : blk_sweep_fn_ntl<false, 0>(P);
 }
 
+template <bool NTL>
+BlkSweepFn blk_part_fn_ntl(int P) {
+    switch (P) {
+        case 2: return k_blk_sweep_part<2, NTL>;
+        case 3: return k_blk_sweep_part<3, NTL>;
+        case 4: return k_blk_sweep_part<4, NTL>;
+        case 5: return k_blk_sweep_part<5, NTL>;
+        case 6: return k_blk_sweep_part<6, NTL>;
+        case 7: return k_blk_sweep_part<7, NTL>;
+        default: return k_blk_sweep_part<8, NTL>;
+    }
+}
+
 template <bool SH>
 BlkStepFn blk_step_fn_sh(int L) {
     switch (L) {
@@ -506,11 +519,10 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     const bool ntl = (int64_t)(s.rows + 1) * s.ld * 8 > kCacheTable;
     // the fixed-chunk form when the grid's wave count is a multiple of the chunks per row
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    // P >= 7: the prefetching fixed form (74 VGPRs) at 7 blocks per CU -- 16384^2: 1094-1105 us
-    // per sweep at P = 8 vs 1139-1144 for the plain fixed form at 8 blocks per CU, 981 vs
-    // 1057-1071 at P = 7 (same box, tools/block_bench.py, profiles/r01_block_sweep_pf.jsonl);
-    // P <= 6: the plain fixed form.  SMX_BLK_PF (experiments): 0 = never prefetch, N >= 2 =
-    // always, at N blocks per CU.
+    // P >= 7: the prefetching fixed form at 7 blocks per CU (16384^2, P = 8: 0.83-0.90 ms per
+    // sweep in place with the column-select fast path, tools/sweep_probe.hip,
+    // profiles/r02_sweep_probe*.jsonl; 1.09-1.16 ms before it); P <= 6: the plain fixed form.
+    // SMX_BLK_PF (experiments): 0 = never prefetch, N >= 2 = always, at N blocks per CU.
     static const int pf_env = [] {
         const char* e = getenv("SMX_BLK_PF");
         return e ? atoi(e) : -1;
@@ -523,10 +535,17 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
         fn = blk_sweep_fn(P, ntl, 0);
         grid = update_grid(s, (const void*)fn, 0);
     }
+    const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk);
+    const double* mul = reinterpret_cast<const double*>(blk + L.mul);
+    const double* pr = reinterpret_cast<const double*>(blk + L.pr);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, tin, tother, s.ld, s.rows + 1,
-                       s.m + 1, reinterpret_cast<const BlkHdr*>(blk),
-                       reinterpret_cast<const double*>(blk + L.mul),
-                       reinterpret_cast<const double*>(blk + L.pr));
+                       s.m + 1, h, mul, pr);
+    if (P > 1) {   // a block cut short by a terminal outcome (does nothing otherwise)
+        BlkSweepFn part = ntl ? blk_part_fn_ntl<true>(P) : blk_part_fn_ntl<false>(P);
+        const int pgrid = update_grid(s, (const void*)part, 0);
+        hipLaunchKernelGGL(part, dim3(pgrid), dim3(kUpdBlock), 0, st, tin, tother, s.ld,
+                           s.rows + 1, s.m + 1, h, mul, pr);
+    }
     return (int)hipGetLastError();
 }
 
