@@ -360,6 +360,24 @@ int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_
 int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, smx_ctl* ctl,
                        void* blk, int64_t blk_bytes, void* stream);
 
+/* ---- Host engine (no device): the same pick_element / recalculate_matrix on a HOST tableau --
+ * For machines without an MI355X (the reference UI's 2-variable LPs, BASELINE.json configs[0]).
+ * Pointers here are HOST pointers (same layout as the device tableau: row-major fp64, R = n + 1
+ * rows, leading dimension shape->ld, f-row entries j >= flen are padding); synchronous; the
+ * decisions and per-element arithmetic are the device engine's, bit for bit.
+ *   smx_host_select <- SimplexMethod.pick_element (simplex.py:70-141): returns the SMX_* status,
+ *                      rc_out[0..1] = (r, c) of the pivot (r also set for SMX_INCORRECT)
+ *   smx_host_pivot  <- recalculate_matrix after its pick (simplex.py:149-177): Tout from Tin,
+ *                      out of place; -1 for an (r, c) outside the tableau
+ *   smx_host_run    <- get_solution's loop (simplex.py:184-198) for k pivots starting at
+ *                      buf[parity]; the table after d pivots is buf[(parity + d) & 1]; returns
+ *                      the pivots applied, status_out = SMX_IDLE when all k were applied, else
+ *                      the terminal SMX_* outcome; log[2 * d .. 2 * d + 1] = (r, c) of pivot d */
+int smx_host_select(const double* T, const smx_shape* shape, int32_t* rc_out);
+int smx_host_pivot(const double* Tin, double* Tout, const smx_shape* shape, int32_t r, int32_t c);
+int64_t smx_host_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                     int64_t k, int32_t* log, int32_t* status_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,7 @@ static_assert(sizeof(smx_part) == 32, "smx_part layout");
 #include "smx_batch.hpp"
 #include "smx_resident.hpp"
 #include "smx_block.hpp"
+#include "smx_host.hpp"
 
 namespace {
 

@@ -2,7 +2,8 @@
 
 The library is built in-tree by ``csrc/Makefile`` (``__graft_entry__.build()`` runs it).  There
 is no fallback of any kind: if the library is missing or fails to load, importing the engine
-raises, so nothing can silently run on the CPU.
+raises.  The host engine (``smx_host_*``, ``host.py``) is part of the same library and is chosen
+only where no HIP device exists (or on request); a HIP device always gets the HIP kernels.
 """
 from __future__ import annotations
 
@@ -56,6 +57,7 @@ EXPORTS = (
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
+    "smx_host_select", "smx_host_pivot", "smx_host_run",
 )
 
 
@@ -145,6 +147,9 @@ def load():
                             ctypes.c_int),
         "smx_bshard_sweep": ([vp, vp, sp, i32, vp, i64, vp], ctypes.c_int),
         "smx_bshard_publish": ([sp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
+        "smx_host_select": ([vp, sp, vp], ctypes.c_int),
+        "smx_host_pivot": ([vp, vp, sp, i32, i32], ctypes.c_int),
+        "smx_host_run": ([vp, vp, sp, i32, i64, vp, vp], ctypes.c_int64),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -5,8 +5,10 @@ same constructor, attributes, method names, return tuples, snapshot objects and 
 strings, so ``main.py:13`` (``from simplex import SimplexMethod, Error``) and
 ``table_widget.py:7`` (``from simplex import Info``) work unchanged through the ``simplex.py``
 drop-in next to this package.  The tableau lives on the MI355X; every selection and every
-pivot is a HIP kernel (``ops.py`` -> ``libsmx.so``).  There is no CPU fallback: without a
-device, construction raises.
+pivot is a HIP kernel (``ops.py`` -> ``libsmx.so``).  On a machine with no HIP device at all (a
+desktop running the reference UI's 2-variable LPs) the same library's host engine runs the
+loop instead (``host.py``, ``backend == "host"``, bit-identical decisions and arithmetic); a
+machine with an MI355X never takes it unless asked (``device="cpu"``).
 
 Additions (not in the reference, all opt-in): ``step()`` (one pick + pivot), ``solve()``
 (``get_solution`` with an optional pivot cap, or the chained no-history fast path),
@@ -172,8 +174,18 @@ def _dense_from_lists(constraints, function, m):
     return T
 
 
+def _use_host(device) -> bool:
+    """The host engine runs a tableau only on request (``device="cpu"``) or when this machine has
+    no HIP device at all; with an MI355X present every tableau lives in HBM."""
+    if device is not None:
+        return str(device) == "cpu"
+    import torch
+    return not torch.cuda.is_available()
+
+
 class SimplexMethod:
-    """simplex.py:24-199 on an MI355X-resident tableau."""
+    """simplex.py:24-199 on an MI355X-resident tableau (or, on a machine without one, on the
+    host engine of the same library: ``backend == "host"``)."""
 
     def __init__(self, constraints, function, device=None):
         # simplex.py:26-33 (IndexError on an empty constraint list, like the reference)
@@ -192,8 +204,12 @@ class SimplexMethod:
         self._initial = [constraint for constraint in constraints]
         self._initial.append(function)
         self.flen = len(function)
-        self._dev = DeviceTableau(_dense_from_lists(constraints, function, self.m),
-                                  self.n, self.m, self.flen, device=device)
+        dense = _dense_from_lists(constraints, function, self.m)
+        if _use_host(device):
+            from .host import HostTableau
+            self._dev = HostTableau(dense, self.n, self.m, self.flen)
+        else:
+            self._dev = DeviceTableau(dense, self.n, self.m, self.flen, device=device)
         self._pristine = True
         self.pivot_log: list[tuple[int, int]] = []
         self.status = "ready"
@@ -257,6 +273,11 @@ class SimplexMethod:
         self.flen = len(func)
         self._dev.upload(_dense_from_lists(cons, func, self.m))
         self._pristine = True
+
+    @property
+    def backend(self) -> str:
+        """"hip" (the tableau is in HBM, every pivot a HIP kernel) or "host" (no HIP device)."""
+        return "host" if getattr(self._dev, "is_host", False) else "hip"
 
     @property
     def pivots(self) -> int:
@@ -356,6 +377,7 @@ class SimplexMethod:
         returns ``LazyInfo`` snapshots whose tables are materialised on access."""
         if lazy is None:
             lazy = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS
+        lazy = lazy and self.backend == "hip"   # device checkpoints + replay need the device
         if lazy and self.flen in (self.m, self.m + 1) and self.flen >= 2:
             return self._get_solution_lazy(max_pivots, detect_cycles, chunk)
         # every snapshot is a fresh acyclic list of lists: pause the cyclic collector so its
@@ -463,7 +485,7 @@ class SimplexMethod:
             return self.get_solution(max_pivots=max_pivots, detect_cycles=detect_cycles)
         if self.flen not in (self.m, self.m + 1) or self.flen < 2:
             return self._solve_stepwise(max_pivots, detect_cycles)
-        big = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS
+        big = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS and self.backend == "hip"
         hist = History(self, every=1 << 62) if big else None    # one checkpoint: the start
         if big:
             first = LazyInfo(self.row, self.column, hist, self.pivots, None, None, 0, 0, 0)

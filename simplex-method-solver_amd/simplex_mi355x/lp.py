@@ -48,12 +48,25 @@ def dense_rows(kind: str, seed: int, n: int, m: int, row_lo: int = 0, row_hi: in
     if out is None:
         out = np.zeros((row_hi - row_lo, width), dtype=np.float64)
     k0, k1 = row_lo // BLOCK, (row_hi + BLOCK - 1) // BLOCK
-    for k in range(k0, k1):
+
+    def fill(k):
         lo, hi = k * BLOCK, min(n, (k + 1) * BLOCK)
         blk = _block(kind, seed, k, hi - lo, m)
         a, b = max(lo, row_lo), min(hi, row_hi)
         if a < b:
             out[a - row_lo:b - row_lo, :m + 1] = blk[a - lo:b - lo]
+
+    if (row_hi - row_lo) * m < (1 << 24):
+        for k in range(k0, k1):
+            fill(k)
+        return out
+    # every block has its own generator, so the blocks are independent: fill them on threads
+    # (numpy's generators release the GIL; a 65536 x 32768 table: ~38 s -> a few seconds)
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    workers = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(fill, range(k0, k1)))
     return out
 
 

@@ -56,13 +56,16 @@ def test_host_helpers_without_gpu():
     assert L.smx_nparts_for(3, 2) == 1
 
 
-def test_engine_refuses_to_run_without_gpu():
+def test_device_tableau_refuses_to_run_without_gpu():
+    """A device tableau never falls back: asking for the MI355X without one raises; only the
+    explicit host engine (chosen by default when no HIP device exists) runs on the CPU."""
     import torch
     if torch.cuda.is_available():
         pytest.skip("GPU present")
     import simplex
     with pytest.raises(RuntimeError, match="no CPU path"):
-        simplex.SimplexMethod([[1.0, 1.0, -2.0]], [-1.0, -1.0])
+        simplex.SimplexMethod([[1.0, 1.0, -2.0]], [-1.0, -1.0], device="cuda:0")
+    assert simplex.SimplexMethod([[1.0, 1.0, -2.0]], [-1.0, -1.0]).backend == "host"
 
 
 def test_reference_entry_errors_before_device():

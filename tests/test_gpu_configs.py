@@ -1,0 +1,180 @@
+"""GPU parity at BASELINE.json's multi-GPU configs, at their real shapes:
+
+* config 4 -- a 16384 x 16384 tableau row-sharded over 2 and then 4 ranks (block pivots, 8 per
+  sweep, and the one-pivot fused protocol), bit for bit against the unsharded C oracle over a
+  prefix with a ragged last block;
+* config 5 -- a 65536 x 32768 degenerate tableau (both degenerate generators) row-sharded over
+  8 ranks on the block path: a 9-pivot prefix bit for bit against the C oracle, then 200 pivots
+  whose trajectory, cycle report and final table are identical to the unsharded HIP path.
+
+The ranks are simulated in one process on the one GPU of the test box: every rank is its own
+``BlockShardBackend`` / ``HipShardBackend`` (own buffers, own stream), the all-gather is a device
+copy of the concatenated send slots (tests/test_gpu_block_sharded.py), so the very kernels of the
+multi-GPU run see the very bytes an RCCL all-gather would hand them.  Reference semantics:
+/root/reference/src/simplex.py:70-177 (selection + update), :179-199 (the loop).
+Host memory at config 5: the 17.2 GB table, the oracle's two 17.2 GB buffers and one download.
+"""
+from __future__ import annotations
+
+import gc
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+
+
+def _free():
+    import torch
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _rows_equal_on_device(bes, dev, n, m):
+    """Every rank's rows (and its f-row replica) equal the unsharded table's, compared on the
+    device as int64 bit patterns (no 17 GB downloads)."""
+    import torch
+    from simplex_mi355x.sharded import row_range
+    full = dev.cur()
+    C = m + 1
+    for p, be in enumerate(bes):
+        lo, hi = row_range(n, p, len(bes))
+        loc = be.dev.cur()
+        a = loc[:hi - lo, :C].contiguous().view(torch.int64)
+        b = full[lo:hi, :C].contiguous().view(torch.int64)
+        assert torch.equal(a, b), f"rank {p}: rows {lo}..{hi} differ"
+        fa = loc[hi - lo, :m].contiguous().view(torch.int64)
+        fb = full[n, :m].contiguous().view(torch.int64)
+        assert torch.equal(fa, fb), f"rank {p}: f-row replica differs"
+
+
+def _cycle(n, m, log):
+    from simplex_mi355x.basis import BasisTracker
+    tr = BasisTracker(n, m)
+    for r, c in log:
+        if tr.pivot(int(r), int(c)):
+            break
+    return tr.cycle
+
+
+# ----------------------------------------------------------------------------------------------
+# config 4: 16384 x 16384 row-sharded across 2 then 4 ranks
+@pytest.fixture(scope="module")
+def table16k():
+    from simplex_mi355x import lp
+    from oracle import c_oracle
+    n = m = 16383
+    T = lp.dense_tableau("uniform", 0, n, m)
+    k = 11   # one block of 8 + a ragged block of 3
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=16)
+    assert done == k
+    yield T, Tref, log
+    del T, Tref
+    gc.collect()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_config4_block_sharded_16k(table16k, world):
+    """16384^2, 8 pivots per sweep on every rank, 11 pivots (8 + a ragged 3): pivots and the
+    whole table bit for bit against the unsharded C oracle."""
+    from test_gpu_block_sharded import _backends, _lockstep, _result
+    T, Tref, log = table16k
+    n = m = 16383
+    bes = _backends(T, n, m, world, 8)
+    _lockstep(bes, 8, 8)
+    _lockstep(bes, 3, 8)
+    states, logs, tables, full = _result(bes)
+    for s, lg in zip(states, logs):
+        assert s["npivots"] == 11 and not s["term"]
+        assert np.array_equal(lg, log)
+    for t in tables[1:]:
+        assert np.array_equal(t[-1, :m].view(np.int64), tables[0][-1, :m].view(np.int64))
+    assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(full[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+    del bes, full, tables
+    _free()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_config4_one_pivot_sharded_16k(table16k, world):
+    """16384^2 with the one-pivot protocol (fused pack -> all-gather -> fused update per pivot),
+    11 pivots: bit for bit against the C oracle."""
+    from test_gpu_sharded import _simulate
+    T, Tref, log = table16k
+    n = m = 16383
+    states, logs, tables, full, bes = _simulate(T, n, m, 11, world, "fused")
+    for s, lg in zip(states, logs):
+        assert s["npivots"] == 11
+        assert np.array_equal(lg, log)
+    assert np.array_equal(full[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(full[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+    del bes, full, tables
+    _free()
+
+
+# ----------------------------------------------------------------------------------------------
+# config 5: 65536 x 32768 row-sharded across 8 ranks, degenerate / anti-cycling stress
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("kind", ["degenerate", "degenerate_mixed"])
+def test_config5_sharded_65536x32768(kind):
+    from simplex_mi355x import lp
+    from simplex_mi355x.device import DeviceTableau
+    from oracle import c_oracle
+    from test_gpu_block_sharded import _backends, _lockstep
+    n, m, world, P = 65535, 32767, 8, 8
+    T = lp.dense_tableau(kind, 0, n, m)
+    dev = DeviceTableau(T, n, m, m, log_cap=1 << 12)
+    assert dev.block_plan()[1] == P            # the unsharded path runs 8 pivots per sweep too
+    bes = _backends(T, n, m, world, P)
+
+    # 9-pivot prefix (a block of 8 + a ragged 1) against the C oracle, bit for bit
+    k0 = 9
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k0, threads=16)
+    del T
+    gc.collect()
+    dev.run(k0, graph=False)
+    ctl = dev.sync_state()
+    _lockstep(bes, k0, P)
+    assert int(ctl["npivots"]) == done, (int(ctl["npivots"]), done, st)
+    assert np.array_equal(dev.read_log(0, done), log)
+    for be in bes:
+        s = be.state()
+        assert s["npivots"] == done
+        assert np.array_equal(be.log(0, done), log)
+    got = dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+    del got, Tref
+    gc.collect()
+    _rows_equal_on_device(bes, dev, n, m)
+
+    # 200 more pivots: identical trajectory, cycle report and table as the unsharded HIP path
+    k1 = 200
+    dev.run(k1, graph=False)
+    ctl = dev.sync_state()
+    _lockstep(bes, k1, P)
+    total = int(ctl["npivots"])
+    ref_log = dev.read_log(0, total)
+    for be in bes:
+        s = be.state()
+        assert s["npivots"] == total and s["term"] == bool(ctl["term"])
+        if s["term"]:
+            assert s["status"] == int(ctl["sel_status"])
+        assert np.array_equal(be.log(0, total), ref_log)
+    assert total == k0 + k1 or bool(ctl["term"])
+    cyc = _cycle(n, m, ref_log)
+    assert _cycle(n, m, bes[0].log(0, total)) == cyc
+    _rows_equal_on_device(bes, dev, n, m)
+    print(f"config 5 ({kind}): {total} pivots, basis cycle {cyc}")
+    del bes, dev
+    _free()
