@@ -92,6 +92,11 @@ typedef struct smx_shape {
     int32_t nparts; /* select workgroups (smx_part records)                                  */
 } smx_shape;
 
+/* Create (once, reused by every *_run_timed call) at least `events` timing events, so that no
+ * event is created or destroyed inside a caller's timed region; the timed calls grow the pool
+ * themselves when it is too small. */
+int smx_timer_reserve(int32_t events);
+
 /* Library/ABI identification; returns the number of kernels built into the library. */
 int smx_version(char* buf, int len);
 /* Recommended number of select partials for a shape (host-only helper). */

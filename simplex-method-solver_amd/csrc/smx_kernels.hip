@@ -610,10 +610,32 @@ struct Graph {
     hipGraphExec_t exec = nullptr;
 };
 
+// Timing events of the *_run_timed calls: created once (smx_timer_reserve, or on first need) and
+// reused, so no hipEventCreate / hipEventDestroy runs inside a caller's timed region.
+hipEvent_t* g_timer_ev = nullptr;
+size_t g_timer_n = 0;
+
+int timer_events(size_t n, hipEvent_t** out) {
+    if (n > g_timer_n) {
+        hipEvent_t* grown = static_cast<hipEvent_t*>(realloc(g_timer_ev, n * sizeof(hipEvent_t)));
+        if (!grown) return 1;
+        g_timer_ev = grown;
+        for (; g_timer_n < n; ++g_timer_n)
+            if (hipEventCreate(&g_timer_ev[g_timer_n]) != hipSuccess) return 1;
+    }
+    *out = g_timer_ev;
+    return 0;
+}
+
 }  // namespace
 
-// =============================================================================================
 extern "C" {
+
+int smx_timer_reserve(int32_t events) {
+    hipEvent_t* ev;
+    return events < 0 ? (int)hipErrorInvalidValue
+                      : (timer_events((size_t)events, &ev) ? (int)hipErrorOutOfMemory : 0);
+}
 
 int smx_version(char* buf, int len) {
     const char* v = "smx 0.1 gfx950 fp64 (select, finalize, update<single|shard|forced>, reset, "
@@ -713,15 +735,9 @@ int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
         return (int)hipErrorInvalidValue;
     hipStream_t st = S(stream);
     const int p0 = parity & 1;
-    hipEvent_t* ev = new hipEvent_t[2 * (size_t)k + 1];
+    hipEvent_t* ev = nullptr;
     int err = 0;
-    for (int i = 0; i < 2 * k + 1; ++i) {
-        if (hipEventCreate(&ev[i]) != hipSuccess) {
-            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
-            delete[] ev;
-            return (int)hipErrorOutOfMemory;
-        }
-    }
+    if (timer_events((size_t)(2 * k + 1), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * k], st);
     if (g_fused) err = launch_prime(p0 ? buf1 : buf0, *shape, p0, ctl, parts, st);
     for (int step = 0; step < k && !err; ++step) {
@@ -748,8 +764,6 @@ int smx_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
             (void)hipEventElapsedTime(&host_update_ms[step], ev[2 * step], ev[2 * step + 1]);
         (void)hipEventElapsedTime(host_total_ms, ev[2 * k], ev[2 * k - 1]);
     }
-    for (int i = 0; i < 2 * k + 1; ++i) (void)hipEventDestroy(ev[i]);
-    delete[] ev;
     return err;
 }
 
@@ -1089,14 +1103,8 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     if (!shape_ok(shape) || !comm || nranks < 1 || k < 1 || !host_update_ms || !host_total_ms)
         return (int)hipErrorInvalidValue;
     hipStream_t st = S(stream);
-    hipEvent_t* ev = new hipEvent_t[2 * (size_t)k + 1];
-    for (int i = 0; i < 2 * k + 1; ++i) {
-        if (hipEventCreate(&ev[i]) != hipSuccess) {
-            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
-            delete[] ev;
-            return (int)hipErrorOutOfMemory;
-        }
-    }
+    hipEvent_t* ev = nullptr;
+    if (timer_events((size_t)(2 * k + 1), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * k], st);
     int err = 0;
     if (g_fused >= 2)
@@ -1118,8 +1126,6 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
             (void)hipEventElapsedTime(&host_update_ms[step], ev[2 * step], ev[2 * step + 1]);
         (void)hipEventElapsedTime(host_total_ms, ev[2 * k], ev[2 * k - 1]);
     }
-    for (int i = 0; i < 2 * k + 1; ++i) (void)hipEventDestroy(ev[i]);
-    delete[] ev;
     return err;
 }
 
@@ -1282,14 +1288,8 @@ int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
         return (int)hipErrorInvalidValue;
     hipStream_t st = S(stream);
     const int nb = (k + pivots - 1) / pivots;
-    hipEvent_t* ev = new hipEvent_t[2 * (size_t)nb + 2];
-    for (int i = 0; i < 2 * nb + 2; ++i) {
-        if (hipEventCreate(&ev[i]) != hipSuccess) {
-            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
-            delete[] ev;
-            return (int)hipErrorOutOfMemory;
-        }
-    }
+    hipEvent_t* ev = nullptr;
+    if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * nb], st);
     int err = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
                                  static_cast<char*>(blk), log, xhist, log_cap, st, ev);
@@ -1300,8 +1300,6 @@ int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
             (void)hipEventElapsedTime(&host_sweep_ms[b], ev[2 * b], ev[2 * b + 1]);
         (void)hipEventElapsedTime(host_total_ms, ev[2 * nb], ev[2 * nb + 1]);
     }
-    for (int i = 0; i < 2 * nb + 2; ++i) (void)hipEventDestroy(ev[i]);
-    delete[] ev;
     return err;
 }
 
@@ -1365,14 +1363,8 @@ int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int
         return (int)hipErrorInvalidValue;
     hipStream_t st = S(stream);
     const int nb = (k + pivots - 1) / pivots;
-    hipEvent_t* ev = new hipEvent_t[2 * (size_t)nb + 2];
-    for (int i = 0; i < 2 * nb + 2; ++i) {
-        if (hipEventCreate(&ev[i]) != hipSuccess) {
-            for (int j = 0; j < i; ++j) (void)hipEventDestroy(ev[j]);
-            delete[] ev;
-            return (int)hipErrorOutOfMemory;
-        }
-    }
+    hipEvent_t* ev = nullptr;
+    if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * nb], st);
     int err = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
                                  static_cast<char*>(blk), log, nullptr, log_cap, st, ev, send,
@@ -1384,8 +1376,6 @@ int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int
             (void)hipEventElapsedTime(&host_sweep_ms[b], ev[2 * b], ev[2 * b + 1]);
         (void)hipEventElapsedTime(host_total_ms, ev[2 * nb], ev[2 * nb + 1]);
     }
-    for (int i = 0; i < 2 * nb + 2; ++i) (void)hipEventDestroy(ev[i]);
-    delete[] ev;
     return err;
 }
 

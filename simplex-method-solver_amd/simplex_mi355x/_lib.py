@@ -57,7 +57,7 @@ EXPORTS = (
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
-    "smx_host_select", "smx_host_pivot", "smx_host_run",
+    "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
 )
 
 
@@ -150,6 +150,7 @@ def load():
         "smx_host_select": ([vp, sp, vp], ctypes.c_int),
         "smx_host_pivot": ([vp, vp, sp, i32, i32], ctypes.c_int),
         "smx_host_run": ([vp, vp, sp, i32, i64, vp, vp], ctypes.c_int64),
+        "smx_timer_reserve": ([i32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
