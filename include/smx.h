@@ -340,16 +340,20 @@ int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, i
  *   step = 1..pivots: pack(step - 1) -> all-gather send -> recv -> step(step); then sweep(T of
  *   the block, the other buffer) -- in place for an even count, so the table after d pivots is in
  *   buf[(parity0 + d) & 1]; after the last block publish(block count).
- * No x-history on this path (xhist is per-rank); `blk` is smx_bshard_bytes bytes. */
+ * x-history: each rank writes (x1, x2) after every pivot into ITS ring for the label rows it
+ * owns, and 0 for a label that is not basic (simplex.py:60-66); the slot of a basic label owned
+ * by another rank is left untouched -- the host takes each value from the owner of the label's
+ * row (it knows the positions from the pivot log).  `xhist` may be NULL.
+ * `blk` is smx_bshard_bytes bytes. */
 int64_t smx_bshard_bytes(const smx_shape* shape);
 int smx_bshard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
                    int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, double* send,
-                   double* recv, int32_t nranks, void* comm, int32_t* log, int64_t log_cap,
-                   void* stream);
+                   double* recv, int32_t nranks, void* comm, int32_t* log, double* xhist,
+                   int64_t log_cap, void* stream);
 int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
                          int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
                          double* send, double* recv, int32_t nranks, void* comm, int32_t* log,
-                         int64_t log_cap, void* stream, float* host_sweep_ms,
+                         double* xhist, int64_t log_cap, void* stream, float* host_sweep_ms,
                          float* host_total_ms);
 int smx_bshard_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                      void* blk, int64_t blk_bytes, void* stream);
@@ -358,12 +362,45 @@ int smx_bshard_pack(const double* T, const smx_shape* shape, int32_t step, int32
                     void* stream);
 int smx_bshard_step(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
                     int32_t parity, int32_t block, const double* recv, int32_t nranks,
-                    smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log, int64_t log_cap,
-                    void* stream);
+                    smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log, double* xhist,
+                    int64_t log_cap, void* stream);
 int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_t pivots,
                      void* blk, int64_t blk_bytes, void* stream);
 int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, smx_ctl* ctl,
                        void* blk, int64_t blk_bytes, void* stream);
+
+/* ---- row sharding across the devices of ONE process (SimplexMethod(..., devices=[...])) ------
+ * The block protocol of smx_bshard_* for all ranks of a single-process job, driven by one host
+ * thread: every rank is a row block on its own device and stream (the smx_bshard_* buffers of
+ * that rank), and per pivot the ranks exchange their send slots by
+ *   SMX_XCHG_RCCL -- one grouped ncclAllGather over the communicators of smx_mshard_comms
+ *                    (ncclCommInitAll over distinct devices), or
+ *   SMX_XCHG_COPY -- device copies of every send slot into every recv, ordered by events (any
+ *                    devices, also several ranks on ONE device, where RCCL refuses).
+ * Stream-ordered, no host synchronisation; the per-rank state afterwards is exactly what
+ * smx_bshard_run leaves on each rank of a multi-process job. */
+#define SMX_XCHG_RCCL 0
+#define SMX_XCHG_COPY 1
+typedef struct smx_rank {
+    int32_t device;     /* HIP device ordinal of this row block                              */
+    int32_t reserved;
+    void* stream;       /* hipStream_t on that device                                        */
+    double* buf0;       /* ping-pong local tableaux: the rank's rows, then its f-row replica */
+    double* buf1;
+    smx_ctl* ctl;
+    void* blk;          /* smx_bshard_bytes(&shape) bytes                                    */
+    int64_t blk_bytes;
+    double* send;       /* SMX_SHARD_HDR + 2 * ld doubles                                    */
+    double* recv;       /* nranks send slots                                                 */
+    int32_t* log;       /* pivot log ring (may be NULL when log_cap = 0)                     */
+    double* xhist;      /* x-history ring, see smx_bshard_* (may be NULL)                    */
+    int64_t log_cap;
+    void* comm;         /* ncclComm_t of this rank (SMX_XCHG_RCCL), else NULL                */
+    smx_shape shape;    /* the rank's local shape (rows, row0; ld equal on every rank)        */
+} smx_rank;
+int smx_mshard_comms(void** comms_out, int32_t nranks, const int32_t* devices);
+int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
+                   int32_t pivots, int32_t exchange);
 
 /* ---- Host engine (no device): the same pick_element / recalculate_matrix on a HOST tableau --
  * For machines without an MI355X (the reference UI's 2-variable LPs, BASELINE.json configs[0]).

@@ -575,9 +575,9 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                     if (r != ncclSuccess) err = -1000 - (int)r;
                 }
             }
-            if (!err)
+            if (!err)   // sharded: each rank writes the x-history of the label rows it owns
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
-                                      sh ? nullptr : xhist, log_cap, st);
+                                      xhist, log_cap, st);
         }
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
         if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st);
@@ -1342,21 +1342,21 @@ int64_t smx_bshard_bytes(const smx_shape* shape) {
 
 int smx_bshard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
                    int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, double* send,
-                   double* recv, int32_t nranks, void* comm, int32_t* log, int64_t log_cap,
-                   void* stream) {
+                   double* recv, int32_t nranks, void* comm, int32_t* log, double* xhist,
+                   int64_t log_cap, void* stream) {
     if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || !send ||
         !recv || nranks < 1 || !comm || k < 0)
         return (int)hipErrorInvalidValue;
     if (k == 0) return 0;
     return launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
-                              static_cast<char*>(blk), log, nullptr, log_cap, S(stream), nullptr,
+                              static_cast<char*>(blk), log, xhist, log_cap, S(stream), nullptr,
                               send, recv, nranks, reinterpret_cast<ncclComm_t>(comm));
 }
 
 int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
                          int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
                          double* send, double* recv, int32_t nranks, void* comm, int32_t* log,
-                         int64_t log_cap, void* stream, float* host_sweep_ms,
+                         double* xhist, int64_t log_cap, void* stream, float* host_sweep_ms,
                          float* host_total_ms) {
     if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || !send ||
         !recv || nranks < 1 || !comm || k < 1 || !host_sweep_ms || !host_total_ms)
@@ -1367,7 +1367,7 @@ int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int
     if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * nb], st);
     int err = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
-                                 static_cast<char*>(blk), log, nullptr, log_cap, st, ev, send,
+                                 static_cast<char*>(blk), log, xhist, log_cap, st, ev, send,
                                  recv, nranks, reinterpret_cast<ncclComm_t>(comm));
     (void)hipEventRecord(ev[2 * nb + 1], st);
     if (!err) err = (int)hipEventSynchronize(ev[2 * nb + 1]);
@@ -1398,13 +1398,13 @@ int smx_bshard_pack(const double* T, const smx_shape* shape, int32_t step, int32
 
 int smx_bshard_step(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
                     int32_t parity, int32_t block, const double* recv, int32_t nranks,
-                    smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log, int64_t log_cap,
-                    void* stream) {
+                    smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log, double* xhist,
+                    int64_t log_cap, void* stream) {
     if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || !ctl || !recv || nranks < 1 ||
         step < 1 || step > pivots || block < 0)
         return (int)hipErrorInvalidValue;
     return launch_blk_step(true, step, T, *shape, pivots, parity & 1, block, ctl,
-                           blk_ptrs(*shape, static_cast<char*>(blk)), recv, nranks, log, nullptr,
+                           blk_ptrs(*shape, static_cast<char*>(blk)), recv, nranks, log, xhist,
                            log_cap, S(stream));
 }
 
@@ -1423,6 +1423,114 @@ int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, sm
         return (int)hipErrorInvalidValue;
     return launch_blk_publish(*shape, parity & 1, block, ctl,
                               blk_ptrs(*shape, static_cast<char*>(blk)), S(stream));
+}
+
+// ---- single-process multi-device row sharding (smx_mshard_*) --------------------------------
+int smx_mshard_comms(void** comms_out, int32_t nranks, const int32_t* devices) {
+    if (!comms_out || !devices || nranks < 1) return (int)hipErrorInvalidValue;
+    ncclComm_t* c = new ncclComm_t[nranks];
+    const ncclResult_t r = ncclCommInitAll(c, nranks, devices);
+    if (r == ncclSuccess)
+        for (int i = 0; i < nranks; ++i) comms_out[i] = c[i];
+    delete[] c;
+    return r == ncclSuccess ? 0 : -1000 - (int)r;
+}
+
+int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
+                   int32_t pivots, int32_t exchange) {
+    if (!ranks || nranks < 1 || k < 0 || pivots < 1 || pivots > kBlkMax ||
+        (exchange != SMX_XCHG_RCCL && exchange != SMX_XCHG_COPY))
+        return (int)hipErrorInvalidValue;
+    for (int q = 0; q < nranks; ++q) {
+        const smx_rank& r = ranks[q];
+        if (!bshard_args_ok(&r.shape, pivots, r.blk, r.blk_bytes) || !r.buf0 || !r.buf1 ||
+            r.buf0 == r.buf1 || !r.ctl || !r.send || !r.recv || r.shape.ld != ranks[0].shape.ld ||
+            (exchange == SMX_XCHG_RCCL && !r.comm))
+            return (int)hipErrorInvalidValue;
+    }
+    if (k == 0) return 0;
+    int dev0 = 0;
+    (void)hipGetDevice(&dev0);
+    const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)ranks[0].shape.ld;
+    BlkPtrs* bp = new BlkPtrs[nranks];
+    hipEvent_t* ev = new hipEvent_t[2 * (size_t)nranks]();   // copy exchange: packed / received
+    int err = 0;
+    for (int q = 0; q < nranks && !err; ++q) {
+        bp[q] = blk_ptrs(ranks[q].shape, static_cast<char*>(ranks[q].blk));
+        if (exchange == SMX_XCHG_COPY) {
+            err = (int)hipSetDevice(ranks[q].device);
+            if (!err) err = (int)hipEventCreateWithFlags(&ev[2 * q], hipEventDisableTiming);
+            if (!err) err = (int)hipEventCreateWithFlags(&ev[2 * q + 1], hipEventDisableTiming);
+        }
+    }
+    auto on = [&](int q) -> hipStream_t {
+        (void)hipSetDevice(ranks[q].device);
+        return S(ranks[q].stream);
+    };
+    auto buf = [&](int q, int p) { return p ? ranks[q].buf1 : ranks[q].buf0; };
+    for (int q = 0; q < nranks && !err; ++q) {
+        hipStream_t st = on(q);
+        err = launch_blk_prime(buf(q, parity & 1), ranks[q].shape, parity & 1, ranks[q].ctl,
+                               bp[q], st);
+    }
+    int p = parity & 1, done = 0, bn = 0;
+    while (!err && done < k) {
+        const int Pb = (k - done < pivots) ? k - done : pivots;
+        for (int l = 1; l <= Pb && !err; ++l) {
+            for (int q = 0; q < nranks && !err; ++q)
+                err = launch_bsh_pack(l - 1, buf(q, p), ranks[q].shape, Pb, bn, ranks[q].ctl,
+                                      bp[q], ranks[q].send, on(q));
+            if (err) break;
+            if (exchange == SMX_XCHG_RCCL) {   // one grouped all-gather over the communicators
+                ncclResult_t rr = ncclGroupStart();
+                for (int q = 0; q < nranks && rr == ncclSuccess; ++q)
+                    rr = ncclAllGather(ranks[q].send, ranks[q].recv, slot, ncclFloat64,
+                                       reinterpret_cast<ncclComm_t>(ranks[q].comm), on(q));
+                const ncclResult_t re = ncclGroupEnd();
+                if (rr == ncclSuccess) rr = re;
+                if (rr != ncclSuccess) err = -1000 - (int)rr;
+            } else {   // every rank copies every send slot into its recv, ordered by events
+                for (int q = 0; q < nranks && !err; ++q)
+                    err = (int)hipEventRecord(ev[2 * q], on(q));
+                for (int q = 0; q < nranks && !err; ++q) {
+                    hipStream_t st = on(q);
+                    for (int o = 0; o < nranks && !err; ++o)
+                        err = (int)hipStreamWaitEvent(st, ev[2 * o], 0);
+                    for (int o = 0; o < nranks && !err; ++o)
+                        err = (int)hipMemcpyAsync(ranks[q].recv + (size_t)o * slot, ranks[o].send,
+                                                  slot * sizeof(double), hipMemcpyDefault, st);
+                    if (!err) err = (int)hipEventRecord(ev[2 * q + 1], st);
+                }
+                // no rank packs into its send slot again before every rank has copied it
+                for (int q = 0; q < nranks && !err; ++q) {
+                    hipStream_t st = on(q);
+                    for (int o = 0; o < nranks && !err; ++o)
+                        err = (int)hipStreamWaitEvent(st, ev[2 * o + 1], 0);
+                }
+            }
+            for (int q = 0; q < nranks && !err; ++q)
+                err = launch_blk_step(true, l, buf(q, p), ranks[q].shape, Pb, p, bn,
+                                      ranks[q].ctl, bp[q], ranks[q].recv, nranks, ranks[q].log,
+                                      ranks[q].xhist, ranks[q].log_cap, on(q));
+        }
+        for (int q = 0; q < nranks && !err; ++q)
+            err = launch_block_sweep(buf(q, p), buf(q, p ^ 1), ranks[q].shape, Pb,
+                                     static_cast<char*>(ranks[q].blk), bp[q].L, on(q));
+        p = (p + Pb) & 1;
+        done += Pb;
+        ++bn;
+    }
+    for (int q = 0; q < nranks && !err; ++q)
+        err = launch_blk_publish(ranks[q].shape, p, bn, ranks[q].ctl, bp[q], on(q));
+    for (int q = 0; q < 2 * nranks; ++q)
+        if (ev[q]) {
+            (void)hipSetDevice(ranks[q / 2].device);
+            (void)hipEventDestroy(ev[q]);   // released once its last record has completed
+        }
+    delete[] ev;
+    delete[] bp;
+    (void)hipSetDevice(dev0);
+    return err;
 }
 
 }  // extern "C"

@@ -40,6 +40,18 @@ class Shape(ctypes.Structure):
                 ("nparts", ctypes.c_int32)]
 
 
+class Rank(ctypes.Structure):
+    """struct smx_rank (include/smx.h): one row block of a single-process multi-device table."""
+    _fields_ = [("device", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("stream", ctypes.c_void_p), ("buf0", ctypes.c_void_p),
+                ("buf1", ctypes.c_void_p), ("ctl", ctypes.c_void_p), ("blk", ctypes.c_void_p),
+                ("blk_bytes", ctypes.c_int64), ("send", ctypes.c_void_p),
+                ("recv", ctypes.c_void_p), ("log", ctypes.c_void_p), ("xhist", ctypes.c_void_p),
+                ("log_cap", ctypes.c_int64), ("comm", ctypes.c_void_p), ("shape", Shape)]
+
+
+XCHG_RCCL, XCHG_COPY = 0, 1
+
 _lib = None
 
 EXPORTS = (
@@ -58,6 +70,7 @@ EXPORTS = (
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
     "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
+    "smx_mshard_comms", "smx_mshard_run",
 )
 
 
@@ -136,14 +149,15 @@ def load():
         "smx_block_graph_create": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp,
                                     ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "smx_bshard_bytes": ([sp], ctypes.c_int64),
-        "smx_bshard_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, i64,
-                            vp], ctypes.c_int),
+        "smx_bshard_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp, vp,
+                            i64, vp], ctypes.c_int),
         "smx_bshard_run_timed": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp,
-                                  i64, vp, ctypes.POINTER(ctypes.c_float),
+                                  vp, i64, vp, ctypes.POINTER(ctypes.c_float),
                                   ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "smx_bshard_prime": ([vp, sp, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_bshard_pack": ([vp, sp, i32, i32, i32, vp, vp, i64, vp, vp], ctypes.c_int),
-        "smx_bshard_step": ([vp, sp, i32, i32, i32, i32, vp, i32, vp, vp, i64, vp, i64, vp],
+        "smx_bshard_step": ([vp, sp, i32, i32, i32, i32, vp, i32, vp, vp, i64, vp, vp, i64,
+                             vp],
                             ctypes.c_int),
         "smx_bshard_sweep": ([vp, vp, sp, i32, vp, i64, vp], ctypes.c_int),
         "smx_bshard_publish": ([sp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
@@ -151,6 +165,9 @@ def load():
         "smx_host_pivot": ([vp, vp, sp, i32, i32], ctypes.c_int),
         "smx_host_run": ([vp, vp, sp, i32, i64, vp, vp], ctypes.c_int64),
         "smx_timer_reserve": ([i32], ctypes.c_int),
+        "smx_mshard_comms": ([ctypes.POINTER(ctypes.c_void_p), i32, ctypes.POINTER(i32)],
+                             ctypes.c_int),
+        "smx_mshard_run": ([ctypes.POINTER(Rank), i32, i32, i32, i32, i32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -187,7 +187,7 @@ class SimplexMethod:
     """simplex.py:24-199 on an MI355X-resident tableau (or, on a machine without one, on the
     host engine of the same library: ``backend == "host"``)."""
 
-    def __init__(self, constraints, function, device=None):
+    def __init__(self, constraints, function, device=None, devices=None, pivots=None):
         # simplex.py:26-33 (IndexError on an empty constraint list, like the reference)
         self.n = len(constraints)
         self.m = len(constraints[0]) - 1
@@ -205,7 +205,11 @@ class SimplexMethod:
         self._initial.append(function)
         self.flen = len(function)
         dense = _dense_from_lists(constraints, function, self.m)
-        if _use_host(device):
+        if devices is not None:
+            # row sharding behind the same surface: rank p's rows on devices[p] (multi.py)
+            from .multi import MultiTableau
+            self._dev = MultiTableau(dense, self.n, self.m, self.flen, devices, pivots=pivots)
+        elif _use_host(device):
             from .host import HostTableau
             self._dev = HostTableau(dense, self.n, self.m, self.flen)
         else:
@@ -276,8 +280,11 @@ class SimplexMethod:
 
     @property
     def backend(self) -> str:
-        """"hip" (the tableau is in HBM, every pivot a HIP kernel) or "host" (no HIP device)."""
-        return "host" if getattr(self._dev, "is_host", False) else "hip"
+        """"hip" (the tableau is in HBM, every pivot a HIP kernel), "sharded" (row blocks on
+        several devices, ``devices=[...]``) or "host" (no HIP device)."""
+        if getattr(self._dev, "is_host", False):
+            return "host"
+        return "sharded" if hasattr(self._dev, "ranks") else "hip"
 
     @property
     def pivots(self) -> int:
@@ -377,7 +384,7 @@ class SimplexMethod:
         returns ``LazyInfo`` snapshots whose tables are materialised on access."""
         if lazy is None:
             lazy = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS
-        lazy = lazy and self.backend == "hip"   # device checkpoints + replay need the device
+        lazy = lazy and self.backend != "host"   # device checkpoints + replay need a device
         if lazy and self.flen in (self.m, self.m + 1) and self.flen >= 2:
             return self._get_solution_lazy(max_pivots, detect_cycles, chunk)
         # every snapshot is a fresh acyclic list of lists: pause the cyclic collector so its
@@ -485,7 +492,7 @@ class SimplexMethod:
             return self.get_solution(max_pivots=max_pivots, detect_cycles=detect_cycles)
         if self.flen not in (self.m, self.m + 1) or self.flen < 2:
             return self._solve_stepwise(max_pivots, detect_cycles)
-        big = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS and self.backend == "hip"
+        big = (self.n + 1) * (self.m + 1) > self.LAZY_ELEMENTS and self.backend != "host"
         hist = History(self, every=1 << 62) if big else None    # one checkpoint: the start
         if big:
             first = LazyInfo(self.row, self.column, hist, self.pivots, None, None, 0, 0, 0)

@@ -273,7 +273,8 @@ class BlockShardBackend:
         _lib.check(_lib.load().smx_bshard_step(
             d.buf[parity].data_ptr(), ctypes.byref(self._shape), step, pivots, parity, block,
             self.recv.data_ptr(), self.world, d.ctl.data_ptr(), self.blk.data_ptr(),
-            self._nbytes, d.log.data_ptr(), d.log_cap, d.stream.cuda_stream), "smx_bshard_step")
+            self._nbytes, d.log.data_ptr(), d.xhist.data_ptr(), d.log_cap,
+            d.stream.cuda_stream), "smx_bshard_step")
 
     def sweep(self, pivots: int, parity: int) -> None:
         d = self.dev
@@ -296,7 +297,8 @@ class BlockShardBackend:
             d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
             self.pivots, d.ctl.data_ptr(), self.blk.data_ptr(), self._nbytes,
             self.send.data_ptr(), self.recv.data_ptr(), self.world, comm.handle,
-            d.log.data_ptr(), d.log_cap, d.stream.cuda_stream), "smx_bshard_run")
+            d.log.data_ptr(), d.xhist.data_ptr(), d.log_cap, d.stream.cuda_stream),
+            "smx_bshard_run")
         d.step += k
         d._pending = True
 
@@ -310,7 +312,8 @@ class BlockShardBackend:
             d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1, k,
             self.pivots, d.ctl.data_ptr(), self.blk.data_ptr(), self._nbytes,
             self.send.data_ptr(), self.recv.data_ptr(), self.world, comm.handle,
-            d.log.data_ptr(), d.log_cap, d.stream.cuda_stream, sw, ctypes.byref(tot)),
+            d.log.data_ptr(), d.xhist.data_ptr(), d.log_cap, d.stream.cuda_stream, sw,
+            ctypes.byref(tot)),
             "smx_bshard_run_timed")
         d.step += k
         d._pending = True

@@ -8,7 +8,8 @@
   ``recalculate_matrix()``'s (the next print_table and the labels); it raises the reference's
   ValueError strings (simplex.py:89, :139).
 
-Both engines: ``host`` (CPU suite) and ``hip`` (MI355X, -m gpu).
+Every engine: ``host`` (CPU suite), ``hip`` and ``sharded`` (three row blocks,
+``devices=[0, 0, 0]``) on the MI355X (-m gpu).
 """
 from __future__ import annotations
 
@@ -21,16 +22,20 @@ from golden_util import dec, dec_input, load
 
 SURFACE = load("surface.json")
 BACKENDS = [pytest.param("host", id="host"),
-            pytest.param("hip", id="hip", marks=pytest.mark.gpu)]
+            pytest.param("hip", id="hip", marks=pytest.mark.gpu),
+            pytest.param("sharded", id="sharded", marks=pytest.mark.gpu)]
 
 
 def _sm(cons, func, backend):
     import simplex
-    if backend == "hip":
+    if backend in ("hip", "sharded"):
         import torch
         if not torch.cuda.is_available():
             pytest.skip("needs an MI355X")
-        sm = simplex.SimplexMethod([list(r) for r in cons], list(func), device="cuda:0")
+        if backend == "hip":
+            sm = simplex.SimplexMethod([list(r) for r in cons], list(func), device="cuda:0")
+        else:   # three row blocks on the one GPU of the test box (copy exchange)
+            sm = simplex.SimplexMethod([list(r) for r in cons], list(func), devices=[0, 0, 0])
     else:
         sm = simplex.SimplexMethod([list(r) for r in cons], list(func), device="cpu")
     assert sm.backend == backend
