@@ -239,9 +239,10 @@ def run_single(args):
         # sweep on the solver stream (the host stays ahead: ~P+1 launches per ~1.5 ms of work),
         # so the sweep average comes from the timed run itself.
         P = bplan[1]
+        nb = -(-args.steps // P)              # blocks of near-equal size (block_size in libsmx)
+        P_top = -(-args.steps // nb)          # the largest block: the dominant sweep kernel
         # the per-sweep timing events exist before the timed region (no hipEventCreate inside)
-        _lib.check(_lib.load().smx_timer_reserve(2 * (-(-args.steps // P)) + 2),
-                   "smx_timer_reserve")
+        _lib.check(_lib.load().smx_timer_reserve(2 * nb + 2), "smx_timer_reserve")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sw, tot_ms = dev.run_block_timed(args.steps, P)
@@ -249,12 +250,13 @@ def run_single(args):
         wall = time.perf_counter() - t0
         dev_ms = tot_ms
         avg_kernel = float(np.mean(sw)) * 1e-3
-        kernel = f"k_blk_sweep<{P}>"
-        traffic = load_traffic(args.traffic, f"{R}x{C}/k_blk_sweep<{P}>")
-        extra = {"pivots_per_launch": P, "launches": len(sw),
+        kernel = f"k_blk_sweep<{P_top}>"
+        traffic = load_traffic(args.traffic, f"{R}x{C}/k_blk_sweep<{P_top}>")
+        extra = {"pivots_per_launch": args.steps / len(sw), "max_pivots_per_launch": P,
+                 "launches": len(sw),
                  "planner_ms_per_pivot": (tot_ms - float(np.sum(sw))) / args.steps,
-                 "algorithmic_bytes_per_pivot": bytes_per_sweep / P}
-        kernels_per_pivot = (P + 1) / P
+                 "algorithmic_bytes_per_pivot": bytes_per_sweep * len(sw) / args.steps}
+        kernels_per_pivot = (args.steps + len(sw)) / args.steps
     else:
         # the timed region replays one pre-captured hipGraph of K chained pivots (one fused
         # k_update per pivot, or the LDS-resident loop for tableaux that fit on chip); HIP events

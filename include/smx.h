@@ -301,7 +301,7 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
                       unsigned long long* out, void* stream);
 
 /* ---- block pivots: P pivots per HBM sweep ------------------------------------------------
- * k pivots of the get_solution loop (simplex.py:184-198) in blocks of `pivots` (1..8): per block,
+ * k pivots of the get_solution loop (simplex.py:184-198) in blocks of `pivots` (1..16): per block,
  * `pivots` planning steps each decide one pivot (pick_element, simplex.py:70-141) from the block's
  * input table T_k -- every value of T_{k+l} they need is re-derived from T_k with the update's own
  * expression chained l times -- then ONE sweep applies all of them to every element
@@ -312,11 +312,18 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
  * Unsharded tableaux only (row0 = 0, rows = n).  `blk` is device scratch of smx_block_bytes
  * bytes (no initialisation needed).  smx_block_bytes: with *pivots_inout = 0 it asks the
  * library's policy (smx_tune_block: 0 automatic = 6 pivots for tables of 48..256 MiB, 8
- * beyond, 1 never, 2..8 that many) and returns 0 when chains of `shape` would not use blocks; with 1..8 it asks for
+ * beyond, 1 never, 2..16 that many) and returns 0 when chains of `shape` would not use blocks; with 1..16 it asks for
  * that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
  * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
  * entries) and the chain's total. */
 int smx_tune_block(int32_t pivots);
+/* Pipelined block chains (default 1): with more than one block, block b+1 is planned on a second
+ * stream of the library while block b is swept (from block b's input table, every chain prefixed
+ * by block b's pivots), the sweeps work out of place, the ragged block comes first, and a final
+ * settle kernel restores the buf[(parity + d) & 1] convention when a terminal outcome cut the
+ * chain.  0 plans each block on the caller's stream before its sweep.  -1 keeps the setting;
+ * returns the previous one. */
+int smx_tune_block_pipe(int32_t on);
 int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout);
 int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
                   int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log,

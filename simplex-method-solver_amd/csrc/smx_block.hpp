@@ -48,21 +48,33 @@ struct SmxBool {
 // k_blk_step<P> builds the records of the NEXT block's first step (chains of length P from this
 // block's T_k), so a block is P + 1 launches.  A terminal outcome at step D latches ctl->term;
 // the sweep still applies the D pivots decided before it and every later kernel does nothing.
-constexpr int kBlkMax = 8;           // pivots per block (mul row stride)
+//
+// Pipelined chains (LAG): block b+1 is planned WHILE block b is swept, on a second stream, from
+// block b's input table X_b (which that sweep only reads: the sweeps of a pipelined chain work
+// out of place) -- every chain is then prefixed by block b's pp pivots (its plan, kept in the
+// other of two plan slots), so the chain of a value of T_{k_{b+1}+D} has length pp + D.  The
+// planner leaves the critical path: a block costs one sweep instead of one sweep + P planner
+// launches.  Where the final table lands then depends on the blocks actually swept; a last
+// k_blk_settle moves it to buf[(parity + d) & 1] when a terminal outcome cut the chain.
+constexpr int kBlkMax = 16;          // pivots per block (mul row stride)
 constexpr int kBlkSlots = kBlkMax + 2;   // record / cf slots: steps 1..P-1, and two for step 0
 constexpr int kBlkNT = kUpdBlock;    // planner workgroup
 constexpr int kBlkScan = 4 * kBlkNT; // columns per early-exit scan round
 
+// One per plan slot (a pipelined chain alternates two); cfs / loc / np0 are the chain's state and
+// live in slot 0 only (`hs` in the kernels).
 struct BlkHdr {
     int32_t peff;                    // pivots of this block decided so far (the sweep's count)
     int32_t pad0;
     int32_t cfs[kBlkSlots];          // first j < fscan with f[j] < 0 of the step in that slot
     int32_t r[kBlkMax], c[kBlkMax];
     int32_t ok[kBlkMax];             // e inside the fast-division window (fd_prep)
-    int32_t pad1;
+    int32_t loc;                     // buffer index (0/1) of the newest table a sweep wrote
     double e[kBlkMax], y[kBlkMax];   // pivot element and its refined reciprocal (fd_prep)
+    int64_t np0;                     // ctl->npivots when the chain started
 };
-static_assert(sizeof(BlkHdr) <= 512, "block header");
+constexpr int64_t kBlkHdrBytes = 1024;   // one plan slot's header
+static_assert(sizeof(BlkHdr) <= kBlkHdrBytes, "block header");
 
 // record / cf slot of block step l: 1..P-1 their own; step 0 of block number bn (the next block's
 // first step, built by k_blk_step<P>) alternates between two slots, so no launch reads the slot
@@ -71,18 +83,21 @@ __host__ __device__ __forceinline__ int blk_slot(int l, int P, int bn) {
     return l == 0 ? kBlkMax + (bn & 1) : (l == P ? kBlkMax + ((bn + 1) & 1) : l);
 }
 
-// Scratch layout (byte offsets; smx_block_bytes): header | records [kBlkSlots][nparts] |
-// mul [R][kBlkMax] | pr [kBlkMax][ld] | fr [2][ld] (the f-row by step parity)
+// Scratch layout (byte offsets; smx_block_bytes): header [2] | records [kBlkSlots][nparts] |
+// mul [2][R][kBlkMax] | pr [2][kBlkMax][ld] | fr [2][ld] (the f-row by step parity).  The
+// second header / mul / pr (plan slot 1) is used by pipelined chains only.
 struct BlkLayout {
-    int64_t parts, mul, pr, fr, bytes;
+    int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot;
 };
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     BlkLayout L;
-    L.parts = 512;
+    L.parts = 2 * kBlkHdrBytes;
     L.mul = blk_align(L.parts + (int64_t)kBlkSlots * nparts * 32);
-    L.pr = blk_align(L.mul + R * kBlkMax * 8);
-    L.fr = blk_align(L.pr + (int64_t)kBlkMax * ld * 8);
+    L.mul_slot = blk_align(R * kBlkMax * 8);
+    L.pr = L.mul + 2 * L.mul_slot;
+    L.pr_slot = blk_align((int64_t)kBlkMax * ld * 8);
+    L.fr = L.pr + 2 * L.pr_slot;
     L.bytes = blk_align(L.fr + 2 * ld * 8);
     return L;
 }
@@ -99,6 +114,33 @@ __device__ __forceinline__ double blk_chain(double x, int i, int j, const BlkPiv
                                             const double* p, const double* mq) {
 #pragma unroll
     for (int q = 0; q < L; ++q) {
+        const double e = pv.e[q];
+        double num;
+        if (i == pv.r[q]) {
+            num = (j == pv.c[q]) ? 1.0 : -x;
+        } else {
+            const double a = x * e;
+            const double b = p[q] * mq[q];
+            num = (j == pv.c[q]) ? x : (a - b);
+        }
+        x = num / e;
+    }
+    return x;
+}
+
+// Pipelined chains: the previous block's pp pivots, then this block's, as one list of at most
+// 2 * kBlkMax + 1 steps, evaluated by a rolled loop with its operands in LDS (p[q]: pivot-row
+// values at column j, mq[q]: row i's multipliers) -- the same operations in the same order as
+// blk_chain, in a few registers.
+struct BlkPiv2 {
+    int r[2 * kBlkMax + 1], c[2 * kBlkMax + 1];
+    double e[2 * kBlkMax + 1];
+};
+
+__device__ __forceinline__ double blk_chain_rolled(double x, int i, int j, const BlkPiv2& pv,
+                                                   int n, const double* p, const double* mq) {
+#pragma unroll 1
+    for (int q = 0; q < n; ++q) {
         const double e = pv.e[q];
         double num;
         if (i == pv.r[q]) {
@@ -139,12 +181,19 @@ __device__ __forceinline__ double blk_fnew(double x, double pj, int j, int c, do
 }
 
 // Chain start: the f-row of T into fr[parity] and its first negative entry (simplex.py:94-98).
+// Also the chain state: loc = buffer index of T, np0 = the pivot count (even for a stopped chain).
 __global__ __launch_bounds__(1024) void k_blk_prime(const double* __restrict__ T, int64_t ld,
                                                      int rows, int m, int fscan, int parity,
-                                                     const smx_ctl* __restrict__ ctl,
+                                                     int loc, const smx_ctl* __restrict__ ctl,
                                                      BlkHdr* __restrict__ h,
+                                                     BlkHdr* __restrict__ h1,
                                                      double* __restrict__ fr) {
     __shared__ int s_tmp[1024 / kWave];
+    if (threadIdx.x == 0) {
+        h->loc = loc;
+        h->np0 = ctl->npivots;
+        h1->peff = 0;
+    }
     if (ctl->term) return;
     const int C = m + 1;
     const double* f = T + (int64_t)rows * ld;
@@ -334,16 +383,34 @@ __global__ __launch_bounds__(kBlkNT) void k_bsh_pack(
 // fly; SH = true (row-sharded): from the P gathered send slots in `recv` (merge_headers), the
 // pivot row taken from the winning slot.  Pivot rows are LOCAL indices in the header (-1 when
 // another rank owns the row); the log and the labels use global ones.
-template <int L, bool SH>
-__global__ __launch_bounds__(kBlkNT) void k_blk_step(
+// LAG (pipelined chains, unsharded): T is the PREVIOUS block's input table and every chain starts
+// with that block's pp pivots (plan slot hp / mulp / prp); h / mul / pr are this block's slot and
+// hs the chain state (slot 0).  The operands the row pass shares (pivot-row values at the
+// columns it reads, row r's multipliers) sit in LDS, keeping the kernel small enough to run next
+// to a sweep.
+template <int L, bool SH, bool LAG>
+__device__ __forceinline__ void blk_step_body(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int row0,
     int P, int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
-    smx_part* __restrict__ parts, double* __restrict__ mul, double* __restrict__ pr,
-    double* __restrict__ fr, const double* __restrict__ recv, int nranks,
-    int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap) {
+    BlkHdr* __restrict__ hs, smx_part* __restrict__ parts, double* __restrict__ mul,
+    double* __restrict__ pr, double* __restrict__ fr, const double* __restrict__ recv,
+    int nranks, int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,
+    const BlkHdr* __restrict__ hp, const double* __restrict__ mulp,
+    const double* __restrict__ prp, int pp) {
     constexpr int D = L - 1;
     constexpr int NT = kBlkNT;
+    // scan rounds: the pipelined form evaluates one column per thread at a time (its chains carry
+    // twice the operands and it must stay within 72 VGPRs); the others issue all four at once
+    constexpr int SCANU = LAG ? 1 : 4;
+    constexpr int NQ = 2 * kBlkMax + 1;
     __shared__ BlkPiv s_pv;
+    __shared__ double s_col[3][kBlkMax];      // pr_q at columns c, m, cf
+    // LAG: the chain's pivots (previous block's, then this block's), row r's multipliers, the
+    // pr_q values at columns c, m, cf, and one operand row per thread
+    __shared__ BlkPiv2 s_all;
+    __shared__ double s_mrall[NQ];
+    __shared__ double s_colall[3][NQ];
+    __shared__ double s_op[LAG ? NT : 1][NQ];
     __shared__ int s_tmp[NT / kWave];
     __shared__ Decision s_d;
     __shared__ int s_nb, s_c;
@@ -351,13 +418,28 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
     __shared__ double s_e, s_fc, s_pm, s_pa;
     const int tid = threadIdx.x;
     const int b = blockIdx.x, G = gridDim.x;
+    if (!LAG) pp = 0;
     if (ctl->term) {
         if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
         return;
     }
     const int sp = (parity + D) & 1;   // step parity of block step D
     const int C = m + 1;
-    blk_load_pivots(h, D, &s_pv);
+    if constexpr (LAG) {
+        if (tid >= kWave && tid - kWave < pp) {
+            const int q = tid - kWave;
+            s_all.r[q] = hp->r[q];
+            s_all.c[q] = hp->c[q];
+            s_all.e[q] = hp->e[q];
+        }
+        if (tid < D) {
+            s_all.r[pp + tid] = h->r[tid];
+            s_all.c[pp + tid] = h->c[tid];
+            s_all.e[pp + tid] = h->e[tid];
+        }
+    } else {
+        blk_load_pivots(h, D, &s_pv);
+    }
     if (SH) {
         if (tid == 0) {
             const ShardDecision sd = merge_headers(recv, nranks, ld, m, flen);
@@ -374,7 +456,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
         const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * G;
         if (tid < G) rec = slot[tid];
-        const int c = h->cfs[blk_slot(D, P, bn)];
+        const int c = hs->cfs[blk_slot(D, P, bn)];
         const int nb = wave_min_int(rec.p1col);
         const First f = wave_first(First{rec.first, rec.first_v});
         const Cand bb = wave_best(Cand{rec.best_cls, rec.best_i, rec.best_v});
@@ -426,13 +508,30 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
     const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
     const double* prow = SH ? recv + s_off : nullptr;    // T_{k+D}[r][*] (sharded)
     double mqr[kBlkMax];
-    if (!SH) {
+    if constexpr (LAG) {
+        if (tid >= kWave && tid - kWave < pp)
+            s_mrall[tid - kWave] = mulp[(int64_t)r_local * kBlkMax + tid - kWave];
+        if (tid < D) s_mrall[pp + tid] = mul[(int64_t)r_local * kBlkMax + tid];
+        __syncthreads();
+    } else if (!SH) {
 #pragma unroll
         for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)r_local * kBlkMax + q];
     }
     auto prv = [&](int j) -> double {
         if (SH) return prow[j];
-        return blk_prv<D>(T, ld, r_local, j, s_pv, pr, mqr);
+        if constexpr (LAG) {
+            double* op = s_op[LAG ? tid : 0];
+#pragma unroll
+            for (int q = 0; q < kBlkMax; ++q)
+                if (q < pp) op[q] = prp[(int64_t)q * ld + j];
+#pragma unroll
+            for (int q = 0; q < D; ++q) op[pp + q] = pr[(int64_t)q * ld + j];
+            return blk_chain_rolled(T[(int64_t)r_local * ld + j], r_local, j, s_all, pp + D, op,
+                                    s_mrall);
+        }
+        double p[kBlkMax];
+        blk_load_col<D>(pr, ld, j, p);
+        return blk_chain<D>(T[(int64_t)r_local * ld + j], r_local, j, s_pv, p, mqr);
     };
     const double* fo = fr + (int64_t)sp * ld;          // f-row of T_{k+D}
     double* fn = fr + (int64_t)(sp ^ 1) * ld;          // f-row of T_{k+L}
@@ -443,7 +542,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         int p1 = SMX_NONE;
         for (int j0 = 0; j0 < m && p1 == SMX_NONE; j0 += kBlkScan) {
             int mine = SMX_NONE;
-#pragma unroll
+#pragma unroll SCANU
             for (int k = 0; k < 4; ++k) {
                 const int j = j0 + k * NT + tid;
                 if (j < m && prv(j) > 0.0 && j < mine) mine = j;
@@ -480,7 +579,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
     int cf = SMX_NONE;
     for (int j0 = 0; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
         int mine = SMX_NONE;
-#pragma unroll
+#pragma unroll SCANU
         for (int k = 0; k < 4; ++k) {
             const int j = j0 + k * NT + tid;
             if (j < fscan && blk_fnew(fo[j], prv(j), j, c, e, fc) < 0.0 && j < mine) mine = j;
@@ -501,7 +600,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         h->y[D] = fd.y;
         h->ok[D] = fd.ok ? 1 : 0;
         h->peff = D + 1;
-        h->cfs[blk_slot(L, P, bn)] = cf;
+        hs->cfs[blk_slot(L, P, bn)] = cf;
         if (log_cap > 0) {
             log[2 * (kpiv % log_cap)] = r;
             log[2 * (kpiv % log_cap) + 1] = c;
@@ -519,23 +618,43 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
             if (hx1 < 0) xhist[2 * (kpiv % log_cap) + 1] = 0.0;
         }
     }
-    __syncthreads();
-    // step L's pivots in LDS-broadcast form: s_pv[D] = this pivot
-    if (tid == 0) {
-        s_pv.r[D] = r_local;
-        s_pv.c[D] = c;
-        s_pv.e[D] = e;
+    // step L's pivots in LDS-broadcast form: s_pv[D] = this pivot; the pivot rows at the columns
+    // the row pass reads (uniform)
+    if constexpr (LAG) {
+        const int n = pp + D;
+        if (tid == 0) {
+            s_all.r[n] = r_local;
+            s_all.c[n] = c;
+            s_all.e[n] = e;
+            s_colall[1][n] = s_pm;
+            s_colall[2][n] = s_pa;
+        }
+        if (tid >= kWave && tid - kWave < pp) {
+            const int q = tid - kWave;
+            s_colall[0][q] = prp[(int64_t)q * ld + c];
+            s_colall[1][q] = prp[(int64_t)q * ld + m];
+            if (cf != SMX_NONE) s_colall[2][q] = prp[(int64_t)q * ld + cf];
+        }
+        if (tid < D) {
+            s_colall[0][pp + tid] = pr[(int64_t)tid * ld + c];
+            s_colall[1][pp + tid] = pr[(int64_t)tid * ld + m];
+            if (cf != SMX_NONE) s_colall[2][pp + tid] = pr[(int64_t)tid * ld + cf];
+        }
+    } else {
+        if (tid == 0) {
+            s_pv.r[D] = r_local;
+            s_pv.c[D] = c;
+            s_pv.e[D] = e;
+            s_col[1][D] = s_pm;
+            s_col[2][D] = s_pa;
+        }
+        if (tid < D) {
+            s_col[0][tid] = pr[(int64_t)tid * ld + c];
+            s_col[1][tid] = pr[(int64_t)tid * ld + m];
+            if (cf != SMX_NONE) s_col[2][tid] = pr[(int64_t)tid * ld + cf];
+        }
     }
     __syncthreads();
-    // the pivot rows at the columns the row pass reads (uniform)
-    double pc_[kBlkMax], pm_[kBlkMax], pa_[kBlkMax];
-    blk_load_col<D>(pr, ld, c, pc_);
-    blk_load_col<D>(pr, ld, m, pm_);
-    pm_[D] = s_pm;
-    if (cf != SMX_NONE) {
-        blk_load_col<D>(pr, ld, cf, pa_);
-        pa_[D] = s_pa;
-    }
     const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
     // x-history of this pivot: the labels' rows as local indices (their "-b" entries of T_{k+L})
     const int hl0 = hx0 >= row0 && hx0 < row0 + rows ? hx0 - row0 : -1;
@@ -547,21 +666,65 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(
         const double xc = row[c];
         const double xb = row[m];
         const double xa = cf != SMX_NONE ? row[cf] : 0.0;
-        double mq[kBlkMax];
+        double bv, a;
+        if constexpr (LAG) {
+            // row i's multipliers (previous block's, then this block's) in its LDS operand row
+            double* op = s_op[LAG ? tid : 0];
+            const double* mrp = mulp + (int64_t)i * kBlkMax;
 #pragma unroll
-        for (int q = 0; q < D; ++q) mq[q] = mr[q];
-        mq[D] = blk_chain<D>(xc, i, c, s_pv, pc_, mq);   // T_{k+D}[i][c]
-        mr[D] = mq[D];
-        const double bv = blk_chain<L>(xb, i, m, s_pv, pm_, mq);
+            for (int q = 0; q < kBlkMax; ++q)
+                if (q < pp) op[q] = mrp[q];
+#pragma unroll
+            for (int q = 0; q < D; ++q) op[pp + q] = mr[q];
+            const int n = pp + D;
+            const double mc = blk_chain_rolled(xc, i, c, s_all, n, s_colall[0], op);
+            mr[D] = mc;                                              // T_{k+D}[i][c]
+            op[n] = mc;
+            bv = blk_chain_rolled(xb, i, m, s_all, n + 1, s_colall[1], op);
+            a = cf != SMX_NONE ? blk_chain_rolled(xa, i, cf, s_all, n + 1, s_colall[2], op) : 0.0;
+        } else {
+            double mq[kBlkMax];
+#pragma unroll
+            for (int q = 0; q < D; ++q) mq[q] = mr[q];
+            mq[D] = blk_chain<D>(xc, i, c, s_pv, s_col[0], mq);   // T_{k+D}[i][c]
+            mr[D] = mq[D];
+            bv = blk_chain<L>(xb, i, m, s_pv, s_col[1], mq);
+            a = cf != SMX_NONE ? blk_chain<L>(xa, i, cf, s_pv, s_col[2], mq) : 0.0;
+        }
         if (xhist && log_cap > 0) {
             if (i == hl0) xhist[hslot] = bv;
             if (i == hl1) xhist[hslot + 1] = bv;
         }
-        const double a = cf != SMX_NONE ? blk_chain<L>(xa, i, cf, s_pv, pa_, mq) : 0.0;
         blk_rec_add(R, row0 + i, bv, cf != SMX_NONE, a);
     }
     blk_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);
 }
+
+#define SMX_BLK_STEP_PARAMS                                                                         \
+    const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int row0,      \
+        int P, int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,              \
+        BlkHdr* __restrict__ hs, smx_part* __restrict__ parts, double* __restrict__ mul,           \
+        double* __restrict__ pr, double* __restrict__ fr, const double* __restrict__ recv,         \
+        int nranks, int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,        \
+        const BlkHdr* __restrict__ hp, const double* __restrict__ mulp,                            \
+        const double* __restrict__ prp, int pp
+#define SMX_BLK_STEP_ARGS                                                                           \
+    T, ld, rows, m, flen, fscan, row0, P, parity, bn, ctl, h, hs, parts, mul, pr, fr, recv, nranks, \
+        log, xhist, log_cap, hp, mulp, prp, pp
+
+// The planner launches.  The pipelined form runs beside a sweep (5 waves per SIMD of 88 VGPRs at
+// P = 8), so it must fit in the 72 VGPRs per SIMD lane the sweep leaves: its rolled LDS-operand
+// chains hold it at 34-41 (the unrolled register form of k_blk_step: 36-117).
+template <int L, bool SH>
+__global__ __launch_bounds__(kBlkNT) void k_blk_step(SMX_BLK_STEP_PARAMS) {
+    blk_step_body<L, SH, false>(SMX_BLK_STEP_ARGS);
+}
+template <int L>
+__global__ __launch_bounds__(kBlkNT) void k_blk_step_lag(SMX_BLK_STEP_PARAMS) {
+    blk_step_body<L, false, true>(SMX_BLK_STEP_ARGS);
+}
+#undef SMX_BLK_STEP_PARAMS
+#undef SMX_BLK_STEP_ARGS
 
 // The sweep: T_k -> T_{k+P} for every element (P = peff pivots of this block).
 // Exact per element with either division (fd_div's window form is bit-identical inside its
@@ -901,52 +1064,77 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no load in flight at exit
 }
 
+// Output: in place when ipx >= 0 and ipx + (pivots applied) is even, else into b_other; the
+// chain state's loc records which buffer (in_idx = index of b_in) now holds the newest table.
+__device__ __forceinline__ double* blk_out(double* b_in, double* b_other, int ipx, int in_idx,
+                                           int applied, BlkHdr* __restrict__ hs) {
+    const bool inplace = ipx >= 0 && ((ipx + applied) & 1) == 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) hs->loc = inplace ? in_idx : in_idx ^ 1;
+    return inplace ? b_in : b_other;
+}
+
 // The sweep of a block that applied all P of its pivots (h->peff == P; otherwise it does nothing
-// and k_blk_sweep_part handles the block): one body per kernel, so the register allocation is
+// and k_blk_sweep_rest handles the block): one body per kernel, so the register allocation is
 // that body's alone.  FORM 0: generic; 1: the launcher made the wave count a multiple of the
-// chunks per row (blk_sweep_body_fixed); 2: that, with the next batch's loads issued before this
-// batch's arithmetic.  In place when P is even, so the table after d pivots is in
-// buf[(parity + d) & 1].
+// chunks per row (blk_sweep_body_fixed; at P >= 7 with the next batch's loads issued before
+// this batch's arithmetic).  Output per blk_out.
 template <int P, bool NTL, int FORM>
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b_other, int64_t ld,
                                                          int R, int C,
                                                          const BlkHdr* __restrict__ h,
                                                          const double* __restrict__ mul,
-                                                         const double* __restrict__ pr) {
+                                                         const double* __restrict__ pr,
+                                                         BlkHdr* __restrict__ hs, int ipx,
+                                                         int in_idx) {
     if (h->peff != P) return;
-    double* out = (P & 1) ? b_other : b_in;
+    double* out = blk_out(b_in, b_other, ipx, in_idx, P, hs);
     if constexpr (FORM > 0)
-        blk_sweep_body_fixed<P, NTL, FORM == 2>(b_in, out, ld, R, C, h, pr, mul);
+        blk_sweep_body_fixed<P, NTL, (P >= 7)>(b_in, out, ld, R, C, h, pr, mul);
     else
         blk_sweep_body<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
 }
 
-// A block that stopped early (a terminal outcome after peff < P pivots, peff > 0): the generic
-// body for its count; launched after k_blk_sweep<P>, it does nothing when peff is 0 or P.
-template <int PMAX, bool NTL>
-__global__ __launch_bounds__(kUpdBlock) void k_blk_sweep_part(double* b_in, double* b_other,
-                                                              int64_t ld, int R, int C,
+// A block that stopped early (a terminal outcome after 0 < peff < P pivots; once per LP): every
+// element through the peff pivots with the exact division, a rolled loop reading each pivot's
+// operands as it goes -- one small kernel for every count instead of a body per count.
+// Launched after k_blk_sweep<P>; does nothing when peff is 0 or P.
+__global__ __launch_bounds__(kUpdBlock) void k_blk_sweep_rest(double* b_in, double* b_other,
+                                                              int64_t ld, int R, int C, int P,
                                                               const BlkHdr* __restrict__ h,
                                                               const double* __restrict__ mul,
-                                                              const double* __restrict__ pr) {
+                                                              const double* __restrict__ pr,
+                                                              BlkHdr* __restrict__ hs, int ipx,
+                                                              int in_idx) {
     const int peff = h->peff;
-    if (peff <= 0 || peff >= PMAX) return;
-    double* out = (peff & 1) ? b_other : b_in;
-#define SMX_BLK_CASE(n)                                                    \
-    if constexpr (PMAX > n) {                                              \
-        if (peff == n) {                                                   \
-            blk_sweep_body<n, NTL>(b_in, out, ld, R, C, h, pr, mul);       \
-            return;                                                        \
-        }                                                                  \
+    if (peff <= 0 || peff >= P) return;
+    double* out = blk_out(b_in, b_other, ipx, in_idx, peff, hs);
+    const int64_t half = (C + 1) / 2;   // dbl2 units per row (ld is even)
+    const int64_t units = (int64_t)R * half;
+    for (int64_t u = (int64_t)blockIdx.x * kUpdBlock + threadIdx.x; u < units;
+         u += (int64_t)gridDim.x * kUpdBlock) {
+        const int i = (int)(u / half);
+        const int j = (int)(u % half) * 2;
+        double v[2] = {b_in[(int64_t)i * ld + j], j + 1 < C ? b_in[(int64_t)i * ld + j + 1] : 0.0};
+        for (int q = 0; q < peff; ++q) {
+            const int rq = h->r[q], cq = h->c[q];
+            const double eq = h->e[q], mq = mul[(int64_t)i * kBlkMax + q];
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                const int jj = j + hh;
+                double num;
+                if (i == rq) {
+                    num = (jj == cq) ? 1.0 : -v[hh];
+                } else {
+                    const double a = v[hh] * eq;
+                    const double b = pr[(int64_t)q * ld + (jj < C ? jj : j)] * mq;
+                    num = (jj == cq) ? v[hh] : (a - b);
+                }
+                v[hh] = num / eq;
+            }
+        }
+        out[(int64_t)i * ld + j] = v[0];
+        if (j + 1 < C) out[(int64_t)i * ld + j + 1] = v[1];
     }
-    SMX_BLK_CASE(1)
-    SMX_BLK_CASE(2)
-    SMX_BLK_CASE(3)
-    SMX_BLK_CASE(4)
-    SMX_BLK_CASE(5)
-    SMX_BLK_CASE(6)
-    SMX_BLK_CASE(7)
-#undef SMX_BLK_CASE
 }
 
 // End of a block chain: the state of the final table into ctl slot `parity` (first negative
@@ -966,6 +1154,26 @@ __global__ __launch_bounds__(kWave) void k_blk_publish(const BlkHdr* __restrict_
         ctl->negb[parity ^ 1] = SMX_NONE;
         ctl->negf[parity ^ 1] = SMX_NONE;
     }
+}
+
+// End of a pipelined chain: the table after the d pivots it applied belongs in
+// buf[(parity + d) & 1] (the ping-pong convention of every chain); the chain's out-of-place sweeps
+// put it there unless a terminal outcome cut the chain short, and then this copies it over
+// (every workgroup returns at once otherwise).
+__global__ __launch_bounds__(kUpdBlock) void k_blk_settle(double* buf0, double* buf1,
+                                                          int64_t ndbl, int parity,
+                                                          const smx_ctl* __restrict__ ctl,
+                                                          const BlkHdr* __restrict__ hs) {
+    const int64_t d = ctl->npivots - hs->np0;
+    const int target = (parity + (int)(d & 1)) & 1;
+    const int loc = hs->loc;
+    if (loc == target) return;
+    const dbl2* src = reinterpret_cast<const dbl2*>(loc ? buf1 : buf0);
+    dbl2* dst = reinterpret_cast<dbl2*>(target ? buf1 : buf0);
+    const int64_t n2 = ndbl / 2;
+    for (int64_t k = (int64_t)blockIdx.x * kUpdBlock + threadIdx.x; k < n2;
+         k += (int64_t)gridDim.x * kUpdBlock)
+        dst[k] = src[k];
 }
 
 }  // namespace

@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <utility>
 #include <string.h>
 
 #include <rccl/rccl.h>
@@ -374,13 +375,18 @@ int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, 
 }
 
 // ---- block pivots (smx_block.hpp) ------------------------------------------------------------
-// smx_tune_block: 0 automatic, 1 never, 2..kBlkMax that many pivots per sweep
-// Automatic policy from tools/block_bench.py (profiles/r01_block_sweep.jsonl): below ~48 MiB the
-// planner's ~15 us per pivot eats the saved traffic (2048^2: block 4 = fused within 1 %); 6
-// pivots per sweep up to 256 MiB (3072^2: 45.8 k pivots/s vs 30.1 k fused), 8 beyond (16384^2).
+// smx_tune_block: 0 automatic, 1 never, 2..kBlkMax that many pivots per sweep (at most: a chain
+// of k pivots is cut into ceil(k / P) blocks of near-equal size, block_size)
+// Automatic policy from tools/block_bench.py (profiles/r01_block_sweep.jsonl,
+// profiles/r02g_block_pivots.jsonl): below ~48 MiB the planner's ~15 us per pivot eats the saved
+// traffic (2048^2: block 4 = fused within 1 %); 6 pivots per sweep up to 256 MiB (3072^2: 45.8 k
+// pivots/s vs 30.1 k fused), 10 up to 1 GiB (8192^2: 43.4 us per pivot at 10, 44.0 at 8, 43.6 at
+// 12), 12 beyond (16384^2: 125.8 us at 12, 129.5 at 10, 128.0 at 14, 139.3 at 8; the sweep is
+// VALU-bound past ~10 pivots: 0.96 / 1.07 / 1.28 / 1.44 / 1.77 ms at 8 / 10 / 12 / 14 / 16).
 int g_block = 0;
 constexpr int64_t kBlockMinTable = 48ll << 20;
 constexpr int64_t kBlockWideTable = 256ll << 20;
+constexpr int64_t kBlockHugeTable = 1ll << 30;
 
 int block_pivots(const smx_shape& s) {
     if (g_block == 1) return 0;
@@ -388,165 +394,162 @@ int block_pivots(const smx_shape& s) {
     if (g_block >= 2) return g_block;
     const int64_t bytes = (int64_t)(s.rows + 1) * s.ld * 8;
     if (bytes < kBlockMinTable) return 0;
-    return bytes >= kBlockWideTable ? 8 : 6;
+    return bytes >= kBlockHugeTable ? 12 : (bytes >= kBlockWideTable ? 10 : 6);
+}
+
+// Pivots of block b when k pivots are cut into ceil(k / P) blocks of near-equal size (the larger
+// ones first): two sweeps of 10 cost less than sweeps of 12 and 8 (1.07 + 1.07 vs 1.28 + 0.96 ms
+// at 16384^2), and a short chain never ends in a mostly idle sweep.
+int block_size(int k, int P, int b) {
+    const int nb = (k + P - 1) / P;
+    const int base = k / nb, extra = k % nb;
+    return base + (b < extra ? 1 : 0);
 }
 
 using BlkSweepFn = void (*)(double*, double*, int64_t, int, int, const BlkHdr*, const double*,
-                           const double*);
+                           const double*, BlkHdr*, int, int);
 using BlkStepFn = void (*)(const double*, int64_t, int, int, int, int, int, int, int, int,
-                           smx_ctl*, BlkHdr*, smx_part*, double*, double*, double*, const double*,
-                           int, int32_t*, double*, int64_t);
+                           smx_ctl*, BlkHdr*, BlkHdr*, smx_part*, double*, double*, double*,
+                           const double*, int, int32_t*, double*, int64_t, const BlkHdr*,
+                           const double*, const double*, int);
 using BshPackFn = void (*)(const double*, int64_t, int, int, int, int, int, const smx_ctl*,
                            const BlkHdr*, const smx_part*, int, const double*, const double*,
                            double*);
 
-template <bool NTL, int FORM>
-BlkSweepFn blk_sweep_fn_ntl(int P) {
-    switch (P) {
-        case 1: return k_blk_sweep<1, NTL, FORM>;
-        case 2: return k_blk_sweep<2, NTL, FORM>;
-        case 3: return k_blk_sweep<3, NTL, FORM>;
-        case 4: return k_blk_sweep<4, NTL, FORM>;
-        case 5: return k_blk_sweep<5, NTL, FORM>;
-        case 6: return k_blk_sweep<6, NTL, FORM>;
-        case 7: return k_blk_sweep<7, NTL, FORM>;
-        default: return k_blk_sweep<8, NTL, FORM>;
-    }
+// Kernel tables by pivot count (1..kBlkMax).  Plain (cache-resident) loads are instantiated up to
+// P = 8 only: larger blocks are for tables far beyond the Infinity Cache.
+template <bool NTL, int FORM, int... Is>
+BlkSweepFn blk_sweep_pick(int P, std::integer_sequence<int, Is...>) {
+    static const BlkSweepFn t[] = {k_blk_sweep<Is + 1, NTL, FORM>...};
+    return t[P - 1];
 }
 
 BlkSweepFn blk_sweep_fn(int P, bool ntl, int form) {
-    if (ntl) {
-        if (form == 2) return blk_sweep_fn_ntl<true, 2>(P);
-        return form ? blk_sweep_fn_ntl<true, 1>(P) : blk_sweep_fn_ntl<true, 0>(P);
-    }
-    if (form == 2) return blk_sweep_fn_ntl<false, 2>(P);
-    return form ? blk_sweep_fn_ntl<false, 1>(P) : blk_sweep_fn_ntl<false, 0>(P);
+    using All = std::make_integer_sequence<int, kBlkMax>;
+    using Low = std::make_integer_sequence<int, 8>;
+    if (ntl || P > 8)
+        return form ? blk_sweep_pick<true, 1>(P, All{}) : blk_sweep_pick<true, 0>(P, All{});
+    return form ? blk_sweep_pick<false, 1>(P, Low{}) : blk_sweep_pick<false, 0>(P, Low{});
 }
 
-template <bool NTL>
-BlkSweepFn blk_part_fn_ntl(int P) {
-    switch (P) {
-        case 2: return k_blk_sweep_part<2, NTL>;
-        case 3: return k_blk_sweep_part<3, NTL>;
-        case 4: return k_blk_sweep_part<4, NTL>;
-        case 5: return k_blk_sweep_part<5, NTL>;
-        case 6: return k_blk_sweep_part<6, NTL>;
-        case 7: return k_blk_sweep_part<7, NTL>;
-        default: return k_blk_sweep_part<8, NTL>;
-    }
+template <bool SH, int... Is>
+BlkStepFn blk_step_pick(int L, std::integer_sequence<int, Is...>) {
+    static const BlkStepFn t[] = {k_blk_step<Is + 1, SH>...};
+    return t[L - 1];
+}
+template <int... Is>
+BlkStepFn blk_lag_pick(int L, std::integer_sequence<int, Is...>) {
+    static const BlkStepFn t[] = {k_blk_step_lag<Is + 1>...};
+    return t[L - 1];
 }
 
-template <bool SH>
+template <bool SH, bool LAG>
 BlkStepFn blk_step_fn_sh(int L) {
-    switch (L) {
-        case 1: return k_blk_step<1, SH>;
-        case 2: return k_blk_step<2, SH>;
-        case 3: return k_blk_step<3, SH>;
-        case 4: return k_blk_step<4, SH>;
-        case 5: return k_blk_step<5, SH>;
-        case 6: return k_blk_step<6, SH>;
-        case 7: return k_blk_step<7, SH>;
-        default: return k_blk_step<8, SH>;
-    }
+    using All = std::make_integer_sequence<int, kBlkMax>;
+    if (LAG) return blk_lag_pick(L, All{});
+    return blk_step_pick<SH>(L, All{});
 }
 
-BshPackFn bsh_pack_fn(int D) {
-    switch (D) {
-        case 0: return k_bsh_pack<0>;
-        case 1: return k_bsh_pack<1>;
-        case 2: return k_bsh_pack<2>;
-        case 3: return k_bsh_pack<3>;
-        case 4: return k_bsh_pack<4>;
-        case 5: return k_bsh_pack<5>;
-        case 6: return k_bsh_pack<6>;
-        default: return k_bsh_pack<7>;
-    }
+template <int... Is>
+BshPackFn bsh_pack_pick(int D, std::integer_sequence<int, Is...>) {
+    static const BshPackFn t[] = {k_bsh_pack<Is>...};
+    return t[D];
 }
+BshPackFn bsh_pack_fn(int D) { return bsh_pack_pick(D, std::make_integer_sequence<int, kBlkMax>{}); }
 
-// Scratch pointers of a block chain
+// Scratch pointers of a block chain (plan slots 0 / 1; h[0] also holds the chain state)
 struct BlkPtrs {
     BlkLayout L;
-    BlkHdr* h;
+    BlkHdr* h[2];
     smx_part* parts;
-    double *mul, *pr, *fr;
+    double *mul[2], *pr[2], *fr;
 };
 BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
     BlkPtrs b;
     b.L = blk_layout(s.rows + 1, s.ld, s.nparts);
-    b.h = reinterpret_cast<BlkHdr*>(blk);
+    for (int k = 0; k < 2; ++k) {
+        b.h[k] = reinterpret_cast<BlkHdr*>(blk + kBlkHdrBytes * k);
+        b.mul[k] = reinterpret_cast<double*>(blk + b.L.mul + k * b.L.mul_slot);
+        b.pr[k] = reinterpret_cast<double*>(blk + b.L.pr + k * b.L.pr_slot);
+    }
     b.parts = reinterpret_cast<smx_part*>(blk + b.L.parts);
-    b.mul = reinterpret_cast<double*>(blk + b.L.mul);
-    b.pr = reinterpret_cast<double*>(blk + b.L.pr);
     b.fr = reinterpret_cast<double*>(blk + b.L.fr);
     return b;
 }
 
-int launch_blk_prime(const double* T, const smx_shape& s, int parity, smx_ctl* ctl,
+// loc: buffer index (0/1) of T
+int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, smx_ctl* ctl,
                      const BlkPtrs& b, hipStream_t st) {
     hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, T, s.ld, s.rows, s.m,
-                       fscan_of(s), parity, (const smx_ctl*)ctl, b.h, b.fr);
+                       fscan_of(s), parity, loc, (const smx_ctl*)ctl, b.h[0], b.h[1], b.fr);
     hipLaunchKernelGGL(k_blk_first, dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
-                       s.row0, (const smx_ctl*)ctl, (const BlkHdr*)b.h, b.parts);
+                       s.row0, (const smx_ctl*)ctl, (const BlkHdr*)b.h[0], b.parts);
     return (int)hipGetLastError();
 }
 
+// One planner launch of block bn (plan slot `slot`).  pp > 0 (pipelined chains): T is the
+// previous block's input table and that block's pp pivots (plan slot slot ^ 1) prefix every chain.
 int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, int parity,
                     int bn, smx_ctl* ctl, const BlkPtrs& b, const double* recv, int nranks,
-                    int32_t* log, double* xhist, int64_t log_cap, hipStream_t st) {
-    BlkStepFn fn = sh ? blk_step_fn_sh<true>(L) : blk_step_fn_sh<false>(L);
+                    int32_t* log, double* xhist, int64_t log_cap, hipStream_t st, int slot = 0,
+                    int pp = 0) {
+    BlkStepFn fn = sh ? blk_step_fn_sh<true, false>(L)
+                      : (pp > 0 ? blk_step_fn_sh<false, true>(L) : blk_step_fn_sh<false, false>(L));
+    const int o = slot ^ 1;
     hipLaunchKernelGGL(fn, dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
-                       fscan_of(s), s.row0, P, parity, bn, ctl, b.h, b.parts, b.mul, b.pr, b.fr,
-                       recv, nranks, log, xhist, log_cap);
+                       fscan_of(s), s.row0, P, parity, bn, ctl, b.h[slot], b.h[0], b.parts,
+                       b.mul[slot], b.pr[slot], b.fr, recv, nranks, log, xhist, log_cap,
+                       (const BlkHdr*)b.h[o], (const double*)b.mul[o], (const double*)b.pr[o],
+                       pp);
     return (int)hipGetLastError();
 }
 
 int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
                     const smx_ctl* ctl, const BlkPtrs& b, double* send, hipStream_t st) {
     hipLaunchKernelGGL(bsh_pack_fn(D), dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
-                       s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h, (const smx_part*)b.parts,
-                       s.nparts, (const double*)b.mul, (const double*)b.pr, send);
+                       s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h[0], (const smx_part*)b.parts,
+                       s.nparts, (const double*)b.mul[0], (const double*)b.pr[0], send);
     return (int)hipGetLastError();
 }
 
 int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, const BlkPtrs& b,
                        hipStream_t st) {
-    hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)b.h,
+    hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)b.h[0],
                        (const smx_part*)b.parts, s.nparts, blk_slot(0, 1, bn), parity, ctl);
     return (int)hipGetLastError();
 }
 
+// ipx / in_idx: see blk_out (ipx 0: in place when the pivots applied are even, the layout of the
+// unpipelined chains; -1: never in place); plan slot `slot`.
 int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, char* blk,
-                       const BlkLayout& L, hipStream_t st) {
+                       const BlkLayout& L, hipStream_t st, int slot = 0, int ipx = 0,
+                       int in_idx = 0, int ipx_part = 0) {
     const bool ntl = (int64_t)(s.rows + 1) * s.ld * 8 > kCacheTable;
-    // the fixed-chunk form when the grid's wave count is a multiple of the chunks per row
-    const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    // P >= 7: the prefetching fixed form at 7 blocks per CU (16384^2, P = 8: 0.83-0.90 ms per
-    // sweep in place with the column-select fast path, tools/sweep_probe.hip,
-    // profiles/r02_sweep_probe*.jsonl; 1.09-1.16 ms before it); P <= 6: the plain fixed form.
-    // SMX_BLK_PF (experiments): 0 = never prefetch, N >= 2 = always, at N blocks per CU.
-    static const int pf_env = [] {
-        const char* e = getenv("SMX_BLK_PF");
-        return e ? atoi(e) : -1;
+    // the fixed-chunk form when the grid's wave count is a multiple of the chunks per row, at
+    // the resident block count (occupancy API: P = 8 holds 81 VGPRs -> 5 blocks per CU; asking
+    // for 7 queued 2 of them behind the rest, 932 / 925 vs 918 / 906 us per sweep at 16384^2,
+    // tools/sweep_pmc.py).  SMX_BLK_BPC (experiments): blocks per CU of the fixed form.
+    static const int bpc_env = [] {
+        const char* e = getenv("SMX_BLK_BPC");
+        return e ? atoi(e) : 0;
     }();
-    const bool pf = pf_env < 0 ? P >= 7 : pf_env >= 2;
-    const int bpc = pf ? (pf_env >= 2 ? pf_env : 7) : 0;
-    BlkSweepFn fn = blk_sweep_fn(P, ntl, pf ? 2 : 1);
-    int grid = update_grid(s, (const void*)fn, 0, bpc);
+    const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
+    BlkSweepFn fn = blk_sweep_fn(P, ntl, 1);
+    int grid = update_grid(s, (const void*)fn, 0, bpc_env);
     if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
         fn = blk_sweep_fn(P, ntl, 0);
         grid = update_grid(s, (const void*)fn, 0);
     }
-    const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk);
-    const double* mul = reinterpret_cast<const double*>(blk + L.mul);
-    const double* pr = reinterpret_cast<const double*>(blk + L.pr);
+    BlkHdr* hs = reinterpret_cast<BlkHdr*>(blk);
+    const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk + kBlkHdrBytes * slot);
+    const double* mul = reinterpret_cast<const double*>(blk + L.mul + slot * L.mul_slot);
+    const double* pr = reinterpret_cast<const double*>(blk + L.pr + slot * L.pr_slot);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, tin, tother, s.ld, s.rows + 1,
-                       s.m + 1, h, mul, pr);
-    if (P > 1) {   // a block cut short by a terminal outcome (does nothing otherwise)
-        BlkSweepFn part = ntl ? blk_part_fn_ntl<true>(P) : blk_part_fn_ntl<false>(P);
-        const int pgrid = update_grid(s, (const void*)part, 0);
-        hipLaunchKernelGGL(part, dim3(pgrid), dim3(kUpdBlock), 0, st, tin, tother, s.ld,
-                           s.rows + 1, s.m + 1, h, mul, pr);
-    }
+                       s.m + 1, h, mul, pr, hs, ipx, in_idx);
+    if (P > 1)   // a block cut short by a terminal outcome (does nothing otherwise)
+        hipLaunchKernelGGL(k_blk_sweep_rest, dim3(num_cus() * 4), dim3(kUpdBlock), 0, st, tin,
+                           tother, s.ld, s.rows + 1, s.m + 1, P, h, mul, pr, hs, ipx_part,
+                           in_idx);
     return (int)hipGetLastError();
 }
 
@@ -561,10 +564,12 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     const BlkPtrs bp = blk_ptrs(s, blk);
     const bool sh = comm != nullptr;
     const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)s.ld;
-    int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, ctl, bp, st);
+    int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, parity, ctl, bp, st);
     int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
-        const int Pb = (k - done < P) ? k - done : P;
+        // unsharded: balanced blocks; row-sharded: blocks of P and a ragged last one (the layout
+        // the step-wise smx_bshard_* protocol and its drivers use)
+        const int Pb = !sh ? block_size(k, P, bn) : ((k - done < P) ? k - done : P);
         double* tin = p ? buf1 : buf0;
         double* toth = p ? buf0 : buf1;
         for (int l = 1; l <= Pb && !err; ++l) {
@@ -580,7 +585,7 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                                       xhist, log_cap, st);
         }
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
-        if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st);
+        if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st, 0, 0, p);
         if (ev) (void)hipEventRecord(ev[2 * bn + 1], st);
         p = (p + Pb) & 1;
         done += Pb;
@@ -588,6 +593,113 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     }
     if (err) return err;
     return launch_blk_publish(s, p, bn, ctl, bp, st);
+}
+
+// ---- pipelined block chains (unsharded) ------------------------------------------------------
+// smx_tune_block_pipe: 1 plans block b+1 on a second stream while block b is swept;
+// 0 (default) plans every block on the solver stream right before its sweep.
+int g_block_pipe = 0;
+
+// The planner stream and the events ordering it against the solver stream, once per device.
+struct BlkPipe {
+    hipStream_t q = nullptr;
+    hipEvent_t fork = nullptr, plan[2] = {nullptr, nullptr}, sweep[2] = {nullptr, nullptr};
+};
+
+int blk_pipe_for(hipStream_t st, BlkPipe** out) {
+    static BlkPipe cache[64];
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
+    BlkPipe& o = cache[dev];
+    if (!o.q) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        hipError_t e = hipSetDevice(dev);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&o.q, hipStreamNonBlocking);
+        hipEvent_t* evs[5] = {&o.fork, &o.plan[0], &o.plan[1], &o.sweep[0], &o.sweep[1]};
+        for (int i = 0; i < 5 && e == hipSuccess; ++i)
+            e = hipEventCreateWithFlags(evs[i], hipEventDisableTiming);
+        (void)hipSetDevice(cur);
+        if (e != hipSuccess) {
+            o.q = nullptr;
+            return (int)e;
+        }
+    }
+    *out = &o;
+    return 0;
+}
+
+// k pivots in blocks of P with the planner off the critical path:
+//   solver stream S: prime; plan block 0 (its steps, from X_0); then per block b:
+//                    [wait plan b] sweep b: X_b -> X_{b+1}, OUT OF PLACE (the planner of block
+//                    b+1 is reading X_b meanwhile); the last block in place when that lands the
+//                    table in buf[(parity + k) & 1]; finally publish + settle
+//   planner stream Q: per block b+1: [wait sweep b-1: X_b complete, plan slot (b+1)&1 free]
+//                    its steps from X_b, every chain prefixed by block b's pivots
+// The ragged block (k not a multiple of P) comes FIRST, so the one exposed planning is the
+// shortest.  ev (optional): 2 timing events per block around its sweep on S.
+int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
+                            int P, smx_ctl* ctl, char* blk, int32_t* log, double* xhist,
+                            int64_t log_cap, hipStream_t st, hipEvent_t* ev = nullptr) {
+    BlkPipe* pp = nullptr;
+    int err = blk_pipe_for(st, &pp);
+    if (err) return err;
+    const BlkPtrs bp = blk_ptrs(s, blk);
+    const int nb = (k + P - 1) / P;
+    const int P0 = k - (nb - 1) * P;
+    auto buf = [&](int idx) { return idx ? buf1 : buf0; };
+    auto hip = [&](hipError_t e) {
+        if (!err && e != hipSuccess) err = (int)e;
+    };
+    err = launch_blk_prime(buf(parity), s, parity, parity, ctl, bp, st);
+    for (int l = 1; l <= P0 && !err; ++l)
+        err = launch_blk_step(false, l, buf(parity), s, P0, parity, 0, ctl, bp, nullptr, 0, log,
+                              xhist, log_cap, st);
+    if (nb > 1) {
+        hip(hipEventRecord(pp->fork, st));
+        hip(hipStreamWaitEvent(pp->q, pp->fork, 0));
+    }
+    int db = 0;   // pivots before block b
+    for (int b = 0; b < nb && !err; ++b) {
+        const int Pb = b == 0 ? P0 : P;
+        const int in_idx = (parity + b) & 1;
+        const bool last = b == nb - 1;
+        const int x = (db - b) & 1;   // blk_out: in place iff x + (pivots applied) is even
+        if (b > 0) hip(hipStreamWaitEvent(st, pp->plan[b & 1], 0));
+        if (ev) hip(hipEventRecord(ev[2 * b], st));
+        if (!err)
+            err = launch_block_sweep(buf(in_idx), buf(in_idx ^ 1), s, Pb, blk, bp.L, st, b & 1,
+                                     last ? x : -1, in_idx, x);
+        if (ev) hip(hipEventRecord(ev[2 * b + 1], st));
+        if (!last) {
+            hip(hipEventRecord(pp->sweep[b & 1], st));
+            if (b >= 1) hip(hipStreamWaitEvent(pp->q, pp->sweep[(b - 1) & 1], 0));
+            const int pnext = (parity + db + Pb) & 1;   // pivot parity at block b+1's start
+            for (int l = 1; l <= P && !err; ++l)
+                err = launch_blk_step(false, l, buf(in_idx), s, P, pnext, b + 1, ctl, bp, nullptr,
+                                      0, log, xhist, log_cap, pp->q, (b + 1) & 1, Pb);
+            hip(hipEventRecord(pp->plan[(b + 1) & 1], pp->q));
+        }
+        db += Pb;
+    }
+    if (err) return err;
+    err = launch_blk_publish(s, (parity + k) & 1, nb, ctl, bp, st);
+    if (err) return err;
+    hipLaunchKernelGGL(k_blk_settle, dim3(num_cus() * 4), dim3(kUpdBlock), 0, st, buf0, buf1,
+                       (int64_t)(s.rows + 1) * s.ld, parity, (const smx_ctl*)ctl,
+                       (const BlkHdr*)bp.h[0]);
+    return (int)hipGetLastError();
+}
+
+// The block chain of smx_block_run: pipelined when enabled and there is more than one block.
+int launch_block_any(double* buf0, double* buf1, const smx_shape& s, int parity, int k, int P,
+                     smx_ctl* ctl, char* blk, int32_t* log, double* xhist, int64_t log_cap,
+                     hipStream_t st, hipEvent_t* ev = nullptr) {
+    if (g_block_pipe && k > P)
+        return launch_block_chain_pipe(buf0, buf1, s, parity, k, P, ctl, blk, log, xhist, log_cap,
+                                       st, ev);
+    return launch_block_chain(buf0, buf1, s, parity, k, P, ctl, blk, log, xhist, log_cap, st, ev);
 }
 
 bool block_args_ok(const smx_shape* shape, int k, int P, const void* blk, int64_t blk_bytes) {
@@ -1253,6 +1365,12 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
     return (int)hipGetLastError();
 }
 
+int smx_tune_block_pipe(int32_t on) {
+    const int prev = g_block_pipe;
+    if (on >= 0) g_block_pipe = on ? 1 : 0;
+    return prev;
+}
+
 int smx_tune_block(int32_t pivots) {
     const int prev = g_block;
     if (pivots >= 0) g_block = pivots > kBlkMax ? kBlkMax : pivots;
@@ -1275,8 +1393,8 @@ int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
     if (!block_args_ok(shape, k, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl)
         return (int)hipErrorInvalidValue;
     if (k == 0) return 0;
-    return launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
-                              static_cast<char*>(blk), log, xhist, log_cap, S(stream));
+    return launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                            static_cast<char*>(blk), log, xhist, log_cap, S(stream));
 }
 
 int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
@@ -1291,8 +1409,8 @@ int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     hipEvent_t* ev = nullptr;
     if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * nb], st);
-    int err = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
-                                 static_cast<char*>(blk), log, xhist, log_cap, st, ev);
+    int err = launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                               static_cast<char*>(blk), log, xhist, log_cap, st, ev);
     (void)hipEventRecord(ev[2 * nb + 1], st);
     if (!err) err = (int)hipEventSynchronize(ev[2 * nb + 1]);
     if (!err) {
@@ -1317,8 +1435,8 @@ int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, i
         delete g;
         return (int)err;
     }
-    int lerr = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
-                                  static_cast<char*>(blk), log, xhist, log_cap, st);
+    int lerr = launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                                static_cast<char*>(blk), log, xhist, log_cap, st);
     err = hipStreamEndCapture(st, &g->graph);
     if (lerr || err != hipSuccess) {
         if (g->graph) (void)hipGraphDestroy(g->graph);
@@ -1382,8 +1500,8 @@ int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int
 int smx_bshard_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                      void* blk, int64_t blk_bytes, void* stream) {
     if (!bshard_args_ok(shape, 1, blk, blk_bytes) || !ctl) return (int)hipErrorInvalidValue;
-    return launch_blk_prime(T, *shape, parity & 1, ctl, blk_ptrs(*shape, static_cast<char*>(blk)),
-                            S(stream));
+    return launch_blk_prime(T, *shape, parity & 1, parity & 1, ctl,
+                            blk_ptrs(*shape, static_cast<char*>(blk)), S(stream));
 }
 
 int smx_bshard_pack(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
@@ -1470,8 +1588,8 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
     auto buf = [&](int q, int p) { return p ? ranks[q].buf1 : ranks[q].buf0; };
     for (int q = 0; q < nranks && !err; ++q) {
         hipStream_t st = on(q);
-        err = launch_blk_prime(buf(q, parity & 1), ranks[q].shape, parity & 1, ranks[q].ctl,
-                               bp[q], st);
+        err = launch_blk_prime(buf(q, parity & 1), ranks[q].shape, parity & 1, parity & 1,
+                               ranks[q].ctl, bp[q], st);
     }
     int p = parity & 1, done = 0, bn = 0;
     while (!err && done < k) {
@@ -1515,7 +1633,7 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
         }
         for (int q = 0; q < nranks && !err; ++q)
             err = launch_block_sweep(buf(q, p), buf(q, p ^ 1), ranks[q].shape, Pb,
-                                     static_cast<char*>(ranks[q].blk), bp[q].L, on(q));
+                                     static_cast<char*>(ranks[q].blk), bp[q].L, on(q), 0, 0, p);
         p = (p + Pb) & 1;
         done += Pb;
         ++bn;

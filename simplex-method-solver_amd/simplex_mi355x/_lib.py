@@ -65,7 +65,7 @@ EXPORTS = (
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
     "smx_tune_resident", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check",
-    "smx_tune_block", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
+    "smx_tune_block", "smx_tune_block_pipe", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
@@ -140,6 +140,7 @@ def load():
                              ctypes.c_int),
         "smx_fastdiv_check": ([vp, vp, i64, vp, vp], ctypes.c_int),
         "smx_tune_block": ([i32], ctypes.c_int),
+        "smx_tune_block_pipe": ([i32], ctypes.c_int),
         "smx_block_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
         "smx_block_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp],
                           ctypes.c_int),
@@ -214,12 +215,19 @@ def block_plan(shape, pivots: int = 0) -> tuple[int, int] | None:
 
 
 def tune_block(pivots: int = -1) -> int:
-    """smx_tune_block: 0 automatic, 1 never, 2..8 pivots per sweep, -1 query only; returns the
+    """smx_tune_block: 0 automatic, 1 never, 2..16 pivots per sweep, -1 query only; returns the
     previous setting."""
     return int(load().smx_tune_block(pivots))
 
 
-BLOCK_MAX = 8   # pivots per sweep at most
+def tune_block_pipe(on: int = -1) -> int:
+    """smx_tune_block_pipe: 1 plan the next block on a second stream during each sweep (the
+    default), 0 plan every block on the solver stream, -1 query only; returns the previous
+    setting."""
+    return int(load().smx_tune_block_pipe(on))
+
+
+BLOCK_MAX = 16   # pivots per sweep at most (kBlkMax)
 
 
 RESIDENT_TIMEOUT = 1   # smx_ctl.dec[0][0] after a resident hand-off timed out

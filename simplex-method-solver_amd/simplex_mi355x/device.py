@@ -94,7 +94,7 @@ class DeviceTableau:
         self.resident = resident
         self._xch = None
         self._epoch = 0
-        # None: the library's policy (smx_tune_block); 0: never; 1..8: pivots per sweep
+        # None: the library's policy (smx_tune_block); 0: never; 1..16: pivots per sweep
         self.block = block
         self._blk = None
         if not defer_upload:

@@ -69,7 +69,7 @@ class MultiTableau:
         self.n, self.m, self.flen = n, m, flen
         self.rows = n
         self.C = m + 1
-        self.P = int(pivots) if pivots else _lib.BLOCK_MAX
+        self.P = int(pivots) if pivots else 8   # the sharded protocol pays one exchange per pivot
         if not 1 <= self.P <= _lib.BLOCK_MAX:
             raise ValueError(f"pivots per sweep must be 1..{_lib.BLOCK_MAX}")
         self.ranges = [row_range(n, p, P) for p in range(P)]

@@ -1,6 +1,6 @@
 """GPU parity of block pivots (smx_block_run, csrc/smx_block.hpp): P pivots planned from the
 block's input table and applied in one HBM sweep.  Bit-exact against the golden fixtures, the C
-oracle and the one-pivot-per-sweep chain, for every block size 1..8, ragged last blocks,
+oracle and the one-pivot-per-sweep chain, for block sizes 1..16, ragged last blocks,
 terminal outcomes inside a block, the x-history ring and interleaving with host steps.
 """
 from __future__ import annotations
@@ -45,7 +45,7 @@ def _solve(cons, func, cap, chunk):
                 table_hash(last.table))
 
 
-@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("P", [2, 3, 4, 8, 11, 16])
 def test_every_fixture_block_vs_chain_vs_reference(block_mode, P):
     """Every trajectory fixture: block chain == one-pivot chain == the reference's pivots, with
     chunks that end inside and at block boundaries and terminal outcomes inside blocks."""
@@ -78,6 +78,9 @@ def test_every_fixture_block_vs_chain_vs_reference(block_mode, P):
     ("degenerate_mixed", 600, 300, 300, 100, 6),
     ("uniform", 65535, 255, 40, 20, 4),        # very tall
     ("mixed", 255, 65535, 40, 20, 4),          # very wide, phase 1
+    ("uniform", 2047, 2047, 100, 100, 16),     # 16 pivots per sweep, ragged last block
+    ("mixed", 1500, 1100, 160, 80, 13),
+    ("degenerate", 700, 700, 200, 200, 12),
 ])
 def test_block_vs_oracle(block_mode, kind, n, m, k, chunk, P):
     from oracle import c_oracle
@@ -96,7 +99,7 @@ def test_block_vs_oracle(block_mode, kind, n, m, k, chunk, P):
     assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
 
 
-@pytest.mark.parametrize("P", [1, 2, 5, 8])
+@pytest.mark.parametrize("P", [1, 2, 5, 8, 16])
 def test_graph_and_eager_block_chains_agree(block_mode, P):
     from simplex_mi355x import lp
     import simplex
@@ -187,10 +190,11 @@ def test_block_terminal_state_matches_chain(block_mode):
     assert seen > 10
 
 
-@pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 11, 8), (16383, 16383, 9, 8), (3071, 3071, 13, 6)])
+@pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 11, 10), (16383, 16383, 9, 12),
+                                     (16383, 16383, 20, 12), (3071, 3071, 13, 6)])
 def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
-    """BASELINE sizes through the default policy (6 or 8 pivots per sweep), a ragged last
-    block."""
+    """BASELINE sizes through the default policy (6, 10 or 12 pivots per sweep at most, blocks of
+    near-equal size: 11 = 6 + 5, 9 = one block, 20 = 10 + 10, 13 = 5 + 4 + 4)."""
     from simplex_mi355x import lp, _lib
     from simplex_mi355x.device import DeviceTableau
     from oracle import c_oracle
@@ -211,12 +215,14 @@ def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
 def test_block_plan_policy(block_mode):
     from simplex_mi355x import _lib
     block_mode(0)
-    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 8
+    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 12
+    assert _lib.block_plan([8192, 8191, 8191, 8191, 8191, 0, 32])[1] == 10
     assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 6
     assert _lib.block_plan([2048, 2047, 2047, 2047, 2047, 0, 8]) is None    # below 48 MiB
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4]) is None
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 6)[1] == 6
     assert _lib.block_plan([1024, 100, 1023, 1023, 1023, 0, 4], 4) is None  # sharded
-    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 9) is None
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 16)[1] == 16
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 17) is None
     block_mode(1)
     assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64]) is None

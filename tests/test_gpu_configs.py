@@ -134,10 +134,11 @@ def test_config5_sharded_65536x32768(kind):
     n, m, world, P = 65535, 32767, 8, 8
     T = lp.dense_tableau(kind, 0, n, m)
     dev = DeviceTableau(T, n, m, m, log_cap=1 << 12)
-    assert dev.block_plan()[1] == P            # the unsharded path runs 8 pivots per sweep too
+    assert dev.block_plan()[1] == 12           # the unsharded path: up to 12 pivots per sweep
     bes = _backends(T, n, m, world, P)
 
-    # 9-pivot prefix (a block of 8 + a ragged 1) against the C oracle, bit for bit
+    # 9-pivot prefix (sharded: a block of 8 + a ragged 1; unsharded: one block) against the C
+    # oracle, bit for bit
     k0 = 9
     Tref, st, done, log = c_oracle.run(T, n, m, m, k0, threads=16)
     del T

@@ -1,7 +1,7 @@
 """Per-pivot time of block pivots (smx_block_*: P pivots per HBM sweep) vs the fused one-pivot
 chain, on seeded uniform LPs, by tableau size and pivots per sweep.
 
-  python tools/block_bench.py [--sizes 4096,8192,16384] [--pivots 1,2,3,4,6,8] [--k 48]
+  python tools/block_bench.py [--sizes 4096,8192,16384] [--pivots 1,2,3,4,6,8] [--k 48] [--pipe 1,0]
 
 One JSON line per (size, path): us per pivot from HIP events on the solver stream around one
 graph replay of k pivots (after a warm-up replay), the average sweep time of a timed run
@@ -25,6 +25,7 @@ def main() -> None:
     ap.add_argument("--pivots", default="1,2,3,4,5,6,8")
     ap.add_argument("--k", type=int, default=48)
     ap.add_argument("--bpc", type=int, default=0, help="blocks per CU of the sweep (0: library)")
+    ap.add_argument("--pipe", default="1", help="smx_tune_block_pipe settings to compare, e.g. 1,0")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -39,7 +40,10 @@ def main() -> None:
         dev = DeviceTableau(T, n, m, m, block=0)
         k = a.k
         ref_log = ref_tab = None
-        for P in [0] + [int(x) for x in a.pivots.split(",")]:
+        runs = [(0, 1)] + [(int(x), int(pp)) for x in a.pivots.split(",")
+                           for pp in a.pipe.split(",")]
+        for P, pipe in runs:
+            _lib.tune_block_pipe(pipe)
             dev.block = P
             dev.upload(T)
             dev.step = 0
@@ -58,7 +62,8 @@ def main() -> None:
             ctl = dev.sync_state()
             log = dev.read_log(0, int(ctl["npivots"]))
             tab = dev.download().view(np.int64)
-            row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "k": k, "bpc": a.bpc,
+            row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "pipe": pipe, "k": k,
+                   "bpc": a.bpc,
                    "us_per_pivot": ms * 1e3 / k, "pivots_s": k / ms * 1e3,
                    "npivots": int(ctl["npivots"])}
             if P == 0:
