@@ -900,7 +900,7 @@ __device__ __forceinline__ int blk_next_batch(int tb, int t) {
     return best;
 }
 
-template <int P, bool NTL, bool PF>
+template <int P, bool NTL, bool PF, int DEPTH = 1>
 __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* Tout, int64_t ld,
                                                      int R, int C, const BlkHdr* __restrict__ h,
                                                      const double* __restrict__ pr,
@@ -1029,12 +1029,15 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
         }
         return;
     }
-    // PF: the next batch's two loads are issued before this batch's arithmetic, into the other of
-    // two register sets, without branches (row and column clamped into the table; a clamped row's
-    // or lane's values are never stored).  The loads are inline asm with explicit waits: the
-    // compiler's own vmcnt tracking waits for them at the loop edge.  In-order vmcnt (gfx9): before
-    // a set is used, the ops issued after its loads are the previous batch's stores (two, as every
-    // wave holds a lane j < C and only the last batch has no row i1) and the other set's loads.
+    // PF: the loads of the next DEPTH batches are issued before this batch's arithmetic, into a
+    // ring of DEPTH + 1 register sets, without branches (row and column clamped into the table; a
+    // clamped row's or lane's values are never stored).  The loads are inline asm with explicit
+    // waits: the compiler's own vmcnt tracking waits for them at the loop edge.  In-order vmcnt
+    // (gfx9 counts loads and stores): before a set is used, the ops issued after its loads are
+    // the other DEPTH sets' loads (two each) and one batch's two stores per set consumed since
+    // (every wave holds a lane j < C, and only the last batch, after which nothing waits, lacks
+    // row i1) -- 4 * DEPTH in the steady state, fewer for the first sets (the exact count is
+    // waited for: a larger one would let a set be used before its loads land).
     const int jc = min(j, (C - 1) & ~1);
     auto ldc = [&](int row) {
         dbl2 v;
@@ -1045,21 +1048,50 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
             asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
         return v;
     };
-    dbl2 a0 = ldc(base), a1 = ldc(base + qs);
-    dbl2 b0 = ldc(base + 2 * qs), b1 = ldc(base + 3 * qs);
-    asm volatile("s_waitcnt vmcnt(2)" : "+v"(a0), "+v"(a1) :: "memory");
-    int t = 0;
-    for (int i0 = base; i0 < R; i0 += 4 * qs, t += 2) {
-        batch(a0, a1, i0, t);
-        if (i0 + 2 * qs >= R) break;
-        a0 = ldc(i0 + 4 * qs);
-        a1 = ldc(i0 + 5 * qs);
-        asm volatile("s_waitcnt vmcnt(4)" : "+v"(b0), "+v"(b1) :: "memory");
-        batch(b0, b1, i0 + 2 * qs, t + 1);
-        if (i0 + 4 * qs >= R) break;
-        b0 = ldc(i0 + 6 * qs);
-        b1 = ldc(i0 + 7 * qs);
+    if constexpr (DEPTH == 1) {
+        dbl2 a0 = ldc(base), a1 = ldc(base + qs);
+        dbl2 b0 = ldc(base + 2 * qs), b1 = ldc(base + 3 * qs);
+        asm volatile("s_waitcnt vmcnt(2)" : "+v"(a0), "+v"(a1) :: "memory");
+        int t = 0;
+        for (int i0 = base; i0 < R; i0 += 4 * qs, t += 2) {
+            batch(a0, a1, i0, t);
+            if (i0 + 2 * qs >= R) break;
+            a0 = ldc(i0 + 4 * qs);
+            a1 = ldc(i0 + 5 * qs);
+            asm volatile("s_waitcnt vmcnt(4)" : "+v"(b0), "+v"(b1) :: "memory");
+            batch(b0, b1, i0 + 2 * qs, t + 1);
+            if (i0 + 4 * qs >= R) break;
+            b0 = ldc(i0 + 6 * qs);
+            b1 = ldc(i0 + 7 * qs);
+            asm volatile("s_waitcnt vmcnt(4)" : "+v"(a0), "+v"(a1) :: "memory");
+        }
+    } else {
+        static_assert(DEPTH == 2, "prefetch depth 1 or 2");
+        dbl2 a0 = ldc(base), a1 = ldc(base + qs);
+        dbl2 b0 = ldc(base + 2 * qs), b1 = ldc(base + 3 * qs);
+        dbl2 c0 = ldc(base + 4 * qs), c1 = ldc(base + 5 * qs);
         asm volatile("s_waitcnt vmcnt(4)" : "+v"(a0), "+v"(a1) :: "memory");
+        int t = 0;
+        for (int i0 = base; i0 < R; i0 += 6 * qs, t += 3) {
+            batch(a0, a1, i0, t);
+            if (i0 + 2 * qs >= R) break;
+            a0 = ldc(i0 + 6 * qs);
+            a1 = ldc(i0 + 7 * qs);
+            if (t == 0)   // after b's first loads: c's loads, a's stores, a's next loads
+                asm volatile("s_waitcnt vmcnt(6)" : "+v"(b0), "+v"(b1) :: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(8)" : "+v"(b0), "+v"(b1) :: "memory");
+            batch(b0, b1, i0 + 2 * qs, t + 1);
+            if (i0 + 4 * qs >= R) break;
+            b0 = ldc(i0 + 8 * qs);
+            b1 = ldc(i0 + 9 * qs);
+            asm volatile("s_waitcnt vmcnt(8)" : "+v"(c0), "+v"(c1) :: "memory");
+            batch(c0, c1, i0 + 4 * qs, t + 2);
+            if (i0 + 6 * qs >= R) break;
+            c0 = ldc(i0 + 10 * qs);
+            c1 = ldc(i0 + 11 * qs);
+            asm volatile("s_waitcnt vmcnt(8)" : "+v"(a0), "+v"(a1) :: "memory");
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no load in flight at exit
 }
@@ -1075,9 +1107,9 @@ __device__ __forceinline__ double* blk_out(double* b_in, double* b_other, int ip
 
 // The sweep of a block that applied all P of its pivots (h->peff == P; otherwise it does nothing
 // and k_blk_sweep_rest handles the block): one body per kernel, so the register allocation is
-// that body's alone.  FORM 0: generic; 1: the launcher made the wave count a multiple of the
-// chunks per row (blk_sweep_body_fixed; at P >= 7 with the next batch's loads issued before
-// this batch's arithmetic).  Output per blk_out.
+// that body's alone.  FORM 0: generic; 1, 2: the launcher made the wave count a multiple of the
+// chunks per row (blk_sweep_body_fixed; at P >= 7 with the next FORM batches' loads issued
+// before this batch's arithmetic).  Output per blk_out.
 template <int P, bool NTL, int FORM>
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b_other, int64_t ld,
                                                          int R, int C,
@@ -1089,7 +1121,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
     if (h->peff != P) return;
     double* out = blk_out(b_in, b_other, ipx, in_idx, P, hs);
     if constexpr (FORM > 0)
-        blk_sweep_body_fixed<P, NTL, (P >= 7)>(b_in, out, ld, R, C, h, pr, mul);
+        blk_sweep_body_fixed<P, NTL, (P >= 7), FORM>(b_in, out, ld, R, C, h, pr, mul);
     else
         blk_sweep_body<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
 }

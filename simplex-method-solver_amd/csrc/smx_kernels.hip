@@ -424,11 +424,14 @@ BlkSweepFn blk_sweep_pick(int P, std::integer_sequence<int, Is...>) {
     return t[P - 1];
 }
 
+// form 0 generic, 1 fixed, 2 fixed with two batches prefetched (streaming loads only)
 BlkSweepFn blk_sweep_fn(int P, bool ntl, int form) {
     using All = std::make_integer_sequence<int, kBlkMax>;
     using Low = std::make_integer_sequence<int, 8>;
-    if (ntl || P > 8)
+    if (ntl || P > 8) {
+        if (form == 2) return blk_sweep_pick<true, 2>(P, All{});
         return form ? blk_sweep_pick<true, 1>(P, All{}) : blk_sweep_pick<true, 0>(P, All{});
+    }
     return form ? blk_sweep_pick<false, 1>(P, Low{}) : blk_sweep_pick<false, 0>(P, Low{});
 }
 
@@ -533,8 +536,14 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
         const char* e = getenv("SMX_BLK_BPC");
         return e ? atoi(e) : 0;
     }();
+    // SMX_BLK_DEPTH (experiments): batches prefetched by the fixed form at P >= 7 (1 or 2)
+    static const int depth_env = [] {
+        const char* e = getenv("SMX_BLK_DEPTH");
+        return e ? atoi(e) : 0;
+    }();
+    const int depth = depth_env == 2 ? 2 : 1;
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    BlkSweepFn fn = blk_sweep_fn(P, ntl, 1);
+    BlkSweepFn fn = blk_sweep_fn(P, ntl, P >= 7 ? depth : 1);
     int grid = update_grid(s, (const void*)fn, 0, bpc_env);
     if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
         fn = blk_sweep_fn(P, ntl, 0);
