@@ -389,7 +389,7 @@ __global__ __launch_bounds__(kBlkNT) void k_bsh_pack(
 // columns it reads, row r's multipliers) sit in LDS, keeping the kernel small enough to run next
 // to a sweep.
 template <int L, bool SH, bool LAG>
-__device__ __forceinline__ void blk_step_body(
+__device__ __forceinline__ bool blk_step_body(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int row0,
     int P, int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
     BlkHdr* __restrict__ hs, smx_part* __restrict__ parts, double* __restrict__ mul,
@@ -421,7 +421,7 @@ __device__ __forceinline__ void blk_step_body(
     if (!LAG) pp = 0;
     if (ctl->term) {
         if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
-        return;
+        return true;
     }
     const int sp = (parity + D) & 1;   // step parity of block step D
     const int C = m + 1;
@@ -502,7 +502,7 @@ __device__ __forceinline__ void blk_step_body(
     };
     if (d.status != SMX_PIVOT) {
         terminal(d);
-        return;
+        return true;
     }
     const int r = d.r;                                   // global pivot row
     const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
@@ -553,7 +553,7 @@ __device__ __forceinline__ void blk_step_body(
             d.c = SMX_NONE;
             d.status = SMX_INCORRECT;   // simplex.py:88-89
             terminal(d);
-            return;
+            return true;
         }
         d.c = p1;
     }
@@ -698,6 +698,7 @@ __device__ __forceinline__ void blk_step_body(
         blk_rec_add(R, row0 + i, bv, cf != SMX_NONE, a);
     }
     blk_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);
+    return false;
 }
 
 #define SMX_BLK_STEP_PARAMS                                                                         \
@@ -723,6 +724,7 @@ template <int L>
 __global__ __launch_bounds__(kBlkNT) void k_blk_step_lag(SMX_BLK_STEP_PARAMS) {
     blk_step_body<L, false, true>(SMX_BLK_STEP_ARGS);
 }
+
 #undef SMX_BLK_STEP_PARAMS
 #undef SMX_BLK_STEP_ARGS
 

@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <mutex>
 #include <utility>
 #include <string.h>
 
@@ -361,6 +362,31 @@ int launch_resident_kernel(double* buf0, double* buf1, const smx_shape& s, const
     return (int)hipGetLastError();
 }
 
+// k_resident's workgroups wait for each other, so two of its launches must never share the
+// device: with each solver on its own stream, two concurrent chains could split the CUs between
+// them and every hand-off would wait for workgroups that cannot be scheduled (until the 2 s
+// timeout).  Every resident launch therefore waits for the previous one on the same device,
+// whatever stream it came from (an event chain per device; other kernels always finish, so they
+// only delay a resident launch).
+int resident_serialize(hipStream_t st, bool after) {
+    static std::mutex mu;
+    static hipEvent_t last[64] = {};
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!last[dev]) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        hipError_t e = hipSetDevice(dev);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&last[dev], hipEventDisableTiming);
+        (void)hipSetDevice(cur);
+        if (e != hipSuccess) return (int)e;
+        if (!after) return 0;   // no resident launch yet on this device
+    }
+    return (int)(after ? hipEventRecord(last[dev], st) : hipStreamWaitEvent(st, last[dev], 0));
+}
+
 int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
                     smx_ctl* ctl, void* xch, int64_t xch_bytes, uint32_t epoch, int32_t* log,
                     double* xhist, int64_t log_cap, hipStream_t st) {
@@ -370,8 +396,12 @@ int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, 
         return (int)hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(&ctl->dec[0][0], 0, sizeof(int32_t), st);   // no latched timeout
     if (e != hipSuccess) return (int)e;
-    return launch_resident_kernel(buf0, buf1, s, p, parity, k, ctl, static_cast<char*>(xch),
-                                  epoch, log, xhist, log_cap, st);
+    int err = resident_serialize(st, false);
+    if (!err)
+        err = launch_resident_kernel(buf0, buf1, s, p, parity, k, ctl, static_cast<char*>(xch),
+                                     epoch, log, xhist, log_cap, st);
+    if (!err) err = resident_serialize(st, true);
+    return err;
 }
 
 // ---- block pivots (smx_block.hpp) ------------------------------------------------------------

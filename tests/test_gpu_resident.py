@@ -200,3 +200,33 @@ def test_fastdiv_matches_hardware_division():
     inside, bad = (int(x) for x in out.cpu())
     assert bad == 0
     assert inside > num.size // 2
+
+
+def test_two_resident_chains_on_separate_streams(resident_mode):
+    """Two solvers, each on its own stream, enqueue resident chains that overlap in time: every
+    workgroup of a chain must be resident at once (256 of them each at 1023^2), so the library
+    orders resident launches on a device one after the other -- without that the two chains
+    would split the CUs and wait on each other's workgroups until the hand-off timeout.  Both
+    must finish without a timeout and equal the oracle."""
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    from simplex_mi355x.device import DeviceTableau
+    import torch
+    resident_mode(0)
+    n = m = 1023
+    k = 150
+    Ts = [lp.dense_tableau(kind, 21, n, m) for kind in ("uniform", "mixed")]
+    devs = [DeviceTableau(T, n, m, m) for T in Ts]
+    for d in devs:
+        assert d.resident_plan() is not None and d.resident_plan()[1][0] == 256
+    torch.cuda.synchronize()
+    for rnd in range(3):                  # interleaved enqueues, no host sync in between
+        for d in devs:
+            d.run(k // 3, graph=False)
+    for d, T in zip(devs, Ts):
+        ctl = d.sync_state()              # raises on a resident hand-off timeout
+        Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+        assert int(ctl["npivots"]) == done
+        assert np.array_equal(d.read_log(0, done), log)
+        got = d.download()
+        assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))

@@ -25,7 +25,7 @@ def main() -> None:
     ap.add_argument("--pivots", default="1,2,3,4,5,6,8")
     ap.add_argument("--k", type=int, default=48)
     ap.add_argument("--bpc", type=int, default=0, help="blocks per CU of the sweep (0: library)")
-    ap.add_argument("--pipe", default="1", help="smx_tune_block_pipe settings to compare, e.g. 1,0")
+    ap.add_argument("--pipe", default="0", help="smx_tune_block_pipe settings to compare, e.g. 1,0")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -40,7 +40,7 @@ def main() -> None:
         dev = DeviceTableau(T, n, m, m, block=0)
         k = a.k
         ref_log = ref_tab = None
-        runs = [(0, 1)] + [(int(x), int(pp)) for x in a.pivots.split(",")
+        runs = [(0, 0)] + [(int(x), int(pp)) for x in a.pivots.split(",")
                            for pp in a.pipe.split(",")]
         for P, pipe in runs:
             _lib.tune_block_pipe(pipe)
