@@ -84,8 +84,9 @@ __host__ __device__ __forceinline__ int blk_slot(int l, int P, int bn) {
 }
 
 // Scratch layout (byte offsets; smx_block_bytes): header [2] | records [kBlkSlots][nparts] |
-// mul [2][R][kBlkMax] | pr [2][kBlkMax][ld] | fr [2][ld] (the f-row by step parity).  The
-// second header / mul / pr (plan slot 1) is used by pipelined chains only.
+// mul [2][R][kBlkMax] | pr [2][kBlkMax][ld] | fr [2][ld] (the f-row by step parity) | the
+// planner's column cache (blk_step_body).  The second header / mul / pr (plan slot 1) is used by
+// pipelined chains only.
 struct BlkLayout {
     int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot;
 };
@@ -98,7 +99,8 @@ inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     L.pr = L.mul + 2 * L.mul_slot;
     L.pr_slot = blk_align((int64_t)kBlkMax * ld * 8);
     L.fr = L.pr + 2 * L.pr_slot;
-    L.bytes = blk_align(L.fr + 2 * ld * 8);
+    // then the planner's column cache: [R] "-b" column, [2][R] the next records' column
+    L.bytes = blk_align(L.fr + 2 * ld * 8 + 3 * R * 8);
     return L;
 }
 
@@ -659,13 +661,24 @@ __device__ __forceinline__ bool blk_step_body(
     // x-history of this pivot: the labels' rows as local indices (their "-b" entries of T_{k+L})
     const int hl0 = hx0 >= row0 && hx0 < row0 + rows ? hx0 - row0 : -1;
     const int hl1 = hx1 >= row0 && hx1 < row0 + rows ? hx1 - row0 : -1;
+    // Column cache: a column read over all rows is one 8-byte load per row, a DRAM page apart
+    // each, and such reads are most of a step's time (k_blk_first, two of them per row, takes
+    // ~8 us at 16384 rows).  Within a block the base table is fixed, so its "-b" column is read
+    // once (step 0) and the column the next step's records are built on -- the next entering
+    // column in phase 2 -- is kept from the step that read it: one strided column per step
+    // instead of three.
+    double* colm = fr + 2 * ld;
+    double* colc = colm + rows;
+    const bool reuse_c = D > 0 && c == s_c;   // phase 2: c is the column of step D's records
     BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
     for (int i = b * NT + tid; i < rows; i += G * NT) {
         const double* row = T + (int64_t)i * ld;
         double* mr = mul + (int64_t)i * kBlkMax;
-        const double xc = row[c];
-        const double xb = row[m];
+        const double xc = reuse_c ? colc[(int64_t)(D & 1) * rows + i] : row[c];
+        const double xb = D > 0 ? colm[i] : row[m];
         const double xa = cf != SMX_NONE ? row[cf] : 0.0;
+        if (D == 0) colm[i] = xb;
+        if (cf != SMX_NONE) colc[(int64_t)(L & 1) * rows + i] = xa;
         double bv, a;
         if constexpr (LAG) {
             // row i's multipliers (previous block's, then this block's) in its LDS operand row
