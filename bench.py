@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--pivots", type=int, default=8,
                     help="row-sharded path: pivots per sweep (block pivots; 1 = one pivot per "
                          "sweep, the fused one-pivot protocol)")
+    ap.add_argument("--xchg", choices=("auto", "full", "light"), default="auto",
+                    help="row-sharded block path: exchange per pivot (full = all-gather of every "
+                         "rank's header + 2 candidate rows; light = header all-gather + one "
+                         "max all-reduce of the pivot row; auto = light from 4 ranks on)")
     return ap.parse_args()
 
 

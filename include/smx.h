@@ -373,6 +373,24 @@ int smx_bshard_step(const double* T, const smx_shape* shape, int32_t step, int32
                     int64_t log_cap, void* stream);
 int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_t pivots,
                      void* blk, int64_t blk_bytes, void* stream);
+/* The light exchange (smx_tune_shard_xchg): instead of all-gathering the whole send slots, a
+ * driver all-gathers the SMX_SHARD_HDR-double headers only (hdrs = [nranks][SMX_SHARD_HDR]),
+ * calls smx_bshard_pick (every rank: the same decision; the owner of the winning row copies it
+ * into `row`, ld doubles, the others fill it with the bit pattern 0x8000000000000000), reduces
+ * `row` over the ranks with MAX on int64 (an all-reduce: the owner's bits survive), and
+ * decides the step with smx_bshard_step_light.  `rank` = this rank's index in the gather order.
+ * Per pivot and rank: 64 B per rank + one row (all-reduce) instead of 64 B + 2 rows per rank. */
+int smx_bshard_pick(const double* hdrs, const smx_shape* shape, int32_t nranks, int32_t rank,
+                    const double* send, double* row, void* stream);
+int smx_bshard_step_light(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
+                          int32_t parity, int32_t block, const double* hdrs, const double* row,
+                          int32_t nranks, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                          int32_t* log, double* xhist, int64_t log_cap, void* stream);
+/* Exchange of smx_bshard_run / smx_mshard_run (SMX_XCHG_RCCL): -1 automatic (light from 4 ranks
+ * on), 0 full send slots, 1 light; -2 keeps; returns the previous setting.  recv must hold
+ * nranks * (SMX_SHARD_HDR + 2 * ld) doubles either way (the light form uses its first
+ * nranks * SMX_SHARD_HDR + ld). */
+int smx_tune_shard_xchg(int32_t mode);
 int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, smx_ctl* ctl,
                        void* blk, int64_t blk_bytes, void* stream);
 

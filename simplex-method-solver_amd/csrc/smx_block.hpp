@@ -380,6 +380,32 @@ __global__ __launch_bounds__(kBlkNT) void k_bsh_pack(
     }
 }
 
+// Light exchange of the row-sharded protocol: only the headers are all-gathered (SMX_SHARD_HDR
+// doubles per rank, `hdrs` = [nranks][SMX_SHARD_HDR]); every rank reaches the same decision from
+// them, the owner of the winning row copies it (row A or B of its send slot) into `row` and the
+// others fill it with the bit pattern 0x8000000000000000, so ONE all-reduce (max over int64)
+// leaves the owner's row, bit for bit (-0.0 included: it IS that pattern), on every rank.
+__global__ __launch_bounds__(kUpdBlock) void k_bsh_pick(const double* __restrict__ hdrs,
+                                                        int nranks, int64_t ld, int m, int flen,
+                                                        int rank, const double* __restrict__ send,
+                                                        double* __restrict__ row) {
+    __shared__ int s_own;
+    __shared__ int64_t s_within;
+    if (threadIdx.x == 0) {
+        const ShardDecision d = merge_headers_s(hdrs, nranks, ld, m, flen, SMX_SHARD_HDR);
+        const bool mine = d.status == SMX_PIVOT && d.owner == rank;
+        s_own = mine ? 1 : 0;
+        s_within = mine ? d.off - (int64_t)d.owner * SMX_SHARD_HDR : 0;
+    }
+    __syncthreads();
+    const bool own = s_own != 0;
+    const double* src = send + s_within;
+    unsigned long long* out = reinterpret_cast<unsigned long long*>(row);
+    for (int64_t j = (int64_t)blockIdx.x * kUpdBlock + threadIdx.x; j < ld;
+         j += (int64_t)gridDim.x * kUpdBlock)
+        out[j] = own ? (unsigned long long)__double_as_longlong(src[j]) : 0x8000000000000000ull;
+}
+
 // One pivot of the block: decide block step D = L-1 and build the records of step L.
 // SH = false: the decision from the records of step D and the pivot-row values derived on the
 // fly; SH = true (row-sharded): from the P gathered send slots in `recv` (merge_headers), the
@@ -398,7 +424,7 @@ __device__ __forceinline__ bool blk_step_body(
     double* __restrict__ pr, double* __restrict__ fr, const double* __restrict__ recv,
     int nranks, int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,
     const BlkHdr* __restrict__ hp, const double* __restrict__ mulp,
-    const double* __restrict__ prp, int pp) {
+    const double* __restrict__ prp, int pp, const double* __restrict__ xrow, int64_t xslot) {
     constexpr int D = L - 1;
     constexpr int NT = kBlkNT;
     // scan rounds: the pipelined form evaluates one column per thread at a time (its chains carry
@@ -444,9 +470,11 @@ __device__ __forceinline__ bool blk_step_body(
     }
     if (SH) {
         if (tid == 0) {
-            const ShardDecision sd = merge_headers(recv, nranks, ld, m, flen);
+            // full exchange: recv = the gathered send slots; light (xslot = SMX_SHARD_HDR): recv
+            // = the gathered headers and xrow = the pivot row (k_bsh_pick + max all-reduce)
+            const int64_t slot = xslot > 0 ? xslot : SMX_SHARD_HDR + 2 * ld;
+            const ShardDecision sd = merge_headers_s(recv, nranks, ld, m, flen, slot);
             int gnb = SMX_NONE;
-            const int64_t slot = SMX_SHARD_HDR + 2 * ld;
             for (int p = 0; p < nranks; ++p) gnb = min(gnb, (int)recv[p * slot]);
             s_d = Decision{sd.status, sd.r, sd.c};
             s_nb = gnb;
@@ -508,7 +536,7 @@ __device__ __forceinline__ bool blk_step_body(
     }
     const int r = d.r;                                   // global pivot row
     const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
-    const double* prow = SH ? recv + s_off : nullptr;    // T_{k+D}[r][*] (sharded)
+    const double* prow = SH ? (xrow ? xrow : recv + s_off) : nullptr;   // T_{k+D}[r][*] (sharded)
     double mqr[kBlkMax];
     if constexpr (LAG) {
         if (tid >= kWave && tid - kWave < pp)
@@ -721,10 +749,10 @@ __device__ __forceinline__ bool blk_step_body(
         double* __restrict__ pr, double* __restrict__ fr, const double* __restrict__ recv,         \
         int nranks, int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,        \
         const BlkHdr* __restrict__ hp, const double* __restrict__ mulp,                            \
-        const double* __restrict__ prp, int pp
+        const double* __restrict__ prp, int pp, const double* __restrict__ xrow, int64_t xslot
 #define SMX_BLK_STEP_ARGS                                                                           \
     T, ld, rows, m, flen, fscan, row0, P, parity, bn, ctl, h, hs, parts, mul, pr, fr, recv, nranks, \
-        log, xhist, log_cap, hp, mulp, prp, pp
+        log, xhist, log_cap, hp, mulp, prp, pp, xrow, xslot
 
 // The planner launches.  The pipelined form runs beside a sweep (5 waves per SIMD of 88 VGPRs at
 // P = 8), so it must fit in the 72 VGPRs per SIMD lane the sweep leaves: its rolled LDS-operand

@@ -147,9 +147,11 @@ struct ShardDecision {
     int64_t off;
 };
 
-__device__ ShardDecision merge_headers(const double* __restrict__ recv, int nranks, int64_t ld,
-                                       int m, int flen) {
-    const int64_t slot = SMX_SHARD_HDR + 2 * ld;
+// `slot`: stride of the gathered headers (the full send slot, SMX_SHARD_HDR + 2 * ld, or just
+// SMX_SHARD_HDR when only the headers were gathered; `off` then still names the row in the
+// owner's own send slot as owner * slot + (SMX_SHARD_HDR or SMX_SHARD_HDR + ld))
+__device__ ShardDecision merge_headers_s(const double* __restrict__ recv, int nranks, int64_t ld,
+                                         int m, int flen, int64_t slot) {
     int gnegb = SMX_NONE, owner_b = -1;
     int gfirst = SMX_NONE, owner_f = -1;
     double fv = 0.0;
@@ -201,6 +203,11 @@ __device__ ShardDecision merge_headers(const double* __restrict__ recv, int nran
         d.off = owner_best * slot + SMX_SHARD_HDR + ld;
     }
     return d;
+}
+
+__device__ ShardDecision merge_headers(const double* __restrict__ recv, int nranks, int64_t ld,
+                                       int m, int flen) {
+    return merge_headers_s(recv, nranks, ld, m, flen, SMX_SHARD_HDR + 2 * ld);
 }
 
 // commit = false: record the selection only (smx_shard_merge, like k_finalize); commit = true:

@@ -441,7 +441,7 @@ using BlkSweepFn = void (*)(double*, double*, int64_t, int, int, const BlkHdr*, 
 using BlkStepFn = void (*)(const double*, int64_t, int, int, int, int, int, int, int, int,
                            smx_ctl*, BlkHdr*, BlkHdr*, smx_part*, double*, double*, double*,
                            const double*, int, int32_t*, double*, int64_t, const BlkHdr*,
-                           const double*, const double*, int);
+                           const double*, const double*, int, const double*, int64_t);
 using BshPackFn = void (*)(const double*, int64_t, int, int, int, int, int, const smx_ctl*,
                            const BlkHdr*, const smx_part*, int, const double*, const double*,
                            double*);
@@ -525,7 +525,7 @@ int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, s
 int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, int parity,
                     int bn, smx_ctl* ctl, const BlkPtrs& b, const double* recv, int nranks,
                     int32_t* log, double* xhist, int64_t log_cap, hipStream_t st, int slot = 0,
-                    int pp = 0) {
+                    int pp = 0, const double* xrow = nullptr, int64_t xslot = 0) {
     BlkStepFn fn = sh ? blk_step_fn_sh<true, false>(L)
                       : (pp > 0 ? blk_step_fn_sh<false, true>(L) : blk_step_fn_sh<false, false>(L));
     const int o = slot ^ 1;
@@ -533,7 +533,24 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
                        fscan_of(s), s.row0, P, parity, bn, ctl, b.h[slot], b.h[0], b.parts,
                        b.mul[slot], b.pr[slot], b.fr, recv, nranks, log, xhist, log_cap,
                        (const BlkHdr*)b.h[o], (const double*)b.mul[o], (const double*)b.pr[o],
-                       pp);
+                       pp, xrow, xslot);
+    return (int)hipGetLastError();
+}
+
+// Row-sharded exchange: SMX_XCHG_FULL all-gathers every rank's send slot (header + rows A, B;
+// SMX_SHARD_HDR + 2 * ld doubles per rank); SMX_XCHG_LIGHT all-gathers the headers only, then
+// k_bsh_pick + ONE max all-reduce of one row (ld doubles) hands the pivot row to every rank.
+// Automatic: light from 4 ranks on (each rank receives 64 B per rank plus ~2 rows per pivot
+// instead of 2 rows per rank: 2.1 MB -> 0.23 MB at 8 ranks of C = 16384, for a second
+// collective's latency), full below.
+int g_shard_xchg = -1;
+bool xchg_light(int nranks) { return g_shard_xchg < 0 ? nranks >= 4 : g_shard_xchg == 1; }
+
+int launch_bsh_pick(const double* hdrs, const smx_shape& s, int nranks, int rank,
+                    const double* send, double* row, hipStream_t st) {
+    const int grid = (int)((s.ld + kUpdBlock - 1) / kUpdBlock);
+    hipLaunchKernelGGL(k_bsh_pick, dim3(grid < 1 ? 1 : grid), dim3(kUpdBlock), 0, st, hdrs,
+                       nranks, s.ld, s.m, s.flen, rank, send, row);
     return (int)hipGetLastError();
 }
 
@@ -603,6 +620,11 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     const BlkPtrs bp = blk_ptrs(s, blk);
     const bool sh = comm != nullptr;
     const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)s.ld;
+    // light exchange: the headers land compact at the start of recv, the pivot row after them
+    const bool light = sh && xchg_light(nranks);
+    int rank = 0;
+    if (light && ncclCommUserRank(comm, &rank) != ncclSuccess) return (int)hipErrorInvalidValue;
+    double* xrow = light ? recv + (size_t)nranks * SMX_SHARD_HDR : nullptr;
     int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, parity, ctl, bp, st);
     int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
@@ -614,14 +636,24 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
         for (int l = 1; l <= Pb && !err; ++l) {
             if (sh) {
                 err = launch_bsh_pack(l - 1, tin, s, Pb, bn, ctl, bp, send, st);
-                if (!err) {
+                if (!err && !light) {
                     const ncclResult_t r = ncclAllGather(send, recv, slot, ncclFloat64, comm, st);
+                    if (r != ncclSuccess) err = -1000 - (int)r;
+                } else if (!err) {
+                    ncclResult_t r = ncclAllGather(send, recv, SMX_SHARD_HDR, ncclFloat64, comm, st);
+                    if (r == ncclSuccess) {
+                        err = launch_bsh_pick(recv, s, nranks, rank, send, xrow, st);
+                        if (!err)
+                            r = ncclAllReduce(xrow, xrow, (size_t)s.ld, ncclInt64, ncclMax, comm,
+                                              st);
+                    }
                     if (r != ncclSuccess) err = -1000 - (int)r;
                 }
             }
             if (!err)   // sharded: each rank writes the x-history of the label rows it owns
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
-                                      xhist, log_cap, st);
+                                      xhist, log_cap, st, 0, 0, xrow,
+                                      light ? (int64_t)SMX_SHARD_HDR : 0);
         }
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
         if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st, 0, 0, p);
@@ -1565,6 +1597,31 @@ int smx_bshard_step(const double* T, const smx_shape* shape, int32_t step, int32
                            log_cap, S(stream));
 }
 
+int smx_tune_shard_xchg(int32_t mode) {
+    const int prev = g_shard_xchg;
+    if (mode >= -1 && mode <= 1) g_shard_xchg = mode;
+    return prev;
+}
+
+int smx_bshard_pick(const double* hdrs, const smx_shape* shape, int32_t nranks, int32_t rank,
+                    const double* send, double* row, void* stream) {
+    if (!shape_ok(shape) || !hdrs || !send || !row || nranks < 1 || rank < 0 || rank >= nranks)
+        return (int)hipErrorInvalidValue;
+    return launch_bsh_pick(hdrs, *shape, nranks, rank, send, row, S(stream));
+}
+
+int smx_bshard_step_light(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,
+                          int32_t parity, int32_t block, const double* hdrs, const double* row,
+                          int32_t nranks, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                          int32_t* log, double* xhist, int64_t log_cap, void* stream) {
+    if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || !ctl || !hdrs || !row || nranks < 1 ||
+        step < 1 || step > pivots || block < 0)
+        return (int)hipErrorInvalidValue;
+    return launch_blk_step(true, step, T, *shape, pivots, parity & 1, block, ctl,
+                           blk_ptrs(*shape, static_cast<char*>(blk)), hdrs, nranks, log, xhist,
+                           log_cap, S(stream), 0, 0, row, SMX_SHARD_HDR);
+}
+
 int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_t pivots,
                      void* blk, int64_t blk_bytes, void* stream) {
     if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || Tin == Tother)
@@ -1625,6 +1682,9 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
         return S(ranks[q].stream);
     };
     auto buf = [&](int q, int p) { return p ? ranks[q].buf1 : ranks[q].buf0; };
+    // light exchange (RCCL only; the copy exchange always moves whole slots)
+    const bool light = exchange == SMX_XCHG_RCCL && xchg_light(nranks);
+    auto xrow = [&](int q) { return ranks[q].recv + (size_t)nranks * SMX_SHARD_HDR; };
     for (int q = 0; q < nranks && !err; ++q) {
         hipStream_t st = on(q);
         err = launch_blk_prime(buf(q, parity & 1), ranks[q].shape, parity & 1, parity & 1,
@@ -1638,7 +1698,28 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                 err = launch_bsh_pack(l - 1, buf(q, p), ranks[q].shape, Pb, bn, ranks[q].ctl,
                                       bp[q], ranks[q].send, on(q));
             if (err) break;
-            if (exchange == SMX_XCHG_RCCL) {   // one grouped all-gather over the communicators
+            if (exchange == SMX_XCHG_RCCL && light) {
+                // grouped header all-gather, every rank's pick, grouped max all-reduce of a row
+                ncclResult_t rr = ncclGroupStart();
+                for (int q = 0; q < nranks && rr == ncclSuccess; ++q)
+                    rr = ncclAllGather(ranks[q].send, ranks[q].recv, SMX_SHARD_HDR, ncclFloat64,
+                                       reinterpret_cast<ncclComm_t>(ranks[q].comm), on(q));
+                ncclResult_t re = ncclGroupEnd();
+                if (rr == ncclSuccess) rr = re;
+                for (int q = 0; q < nranks && rr == ncclSuccess && !err; ++q)
+                    err = launch_bsh_pick(ranks[q].recv, ranks[q].shape, nranks, q, ranks[q].send,
+                                          xrow(q), on(q));
+                if (rr == ncclSuccess && !err) {
+                    rr = ncclGroupStart();
+                    for (int q = 0; q < nranks && rr == ncclSuccess; ++q)
+                        rr = ncclAllReduce(xrow(q), xrow(q), (size_t)ranks[q].shape.ld, ncclInt64,
+                                           ncclMax, reinterpret_cast<ncclComm_t>(ranks[q].comm),
+                                           on(q));
+                    re = ncclGroupEnd();
+                    if (rr == ncclSuccess) rr = re;
+                }
+                if (rr != ncclSuccess) err = -1000 - (int)rr;
+            } else if (exchange == SMX_XCHG_RCCL) {   // one grouped all-gather of the slots
                 ncclResult_t rr = ncclGroupStart();
                 for (int q = 0; q < nranks && rr == ncclSuccess; ++q)
                     rr = ncclAllGather(ranks[q].send, ranks[q].recv, slot, ncclFloat64,
@@ -1668,7 +1749,9 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
             for (int q = 0; q < nranks && !err; ++q)
                 err = launch_blk_step(true, l, buf(q, p), ranks[q].shape, Pb, p, bn,
                                       ranks[q].ctl, bp[q], ranks[q].recv, nranks, ranks[q].log,
-                                      ranks[q].xhist, ranks[q].log_cap, on(q));
+                                      ranks[q].xhist, ranks[q].log_cap, on(q), 0, 0,
+                                      light ? xrow(q) : nullptr,
+                                      light ? (int64_t)SMX_SHARD_HDR : 0);
         }
         for (int q = 0; q < nranks && !err; ++q)
             err = launch_block_sweep(buf(q, p), buf(q, p ^ 1), ranks[q].shape, Pb,

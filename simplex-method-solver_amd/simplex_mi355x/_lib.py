@@ -69,6 +69,7 @@ EXPORTS = (
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
+    "smx_bshard_pick", "smx_bshard_step_light", "smx_tune_shard_xchg",
     "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
     "smx_mshard_comms", "smx_mshard_run",
 )
@@ -161,6 +162,10 @@ def load():
                              vp],
                             ctypes.c_int),
         "smx_bshard_sweep": ([vp, vp, sp, i32, vp, i64, vp], ctypes.c_int),
+        "smx_bshard_pick": ([vp, sp, i32, i32, vp, vp, vp], ctypes.c_int),
+        "smx_bshard_step_light": ([vp, sp, i32, i32, i32, i32, vp, vp, i32, vp, vp, i64, vp, vp,
+                                   i64, vp], ctypes.c_int),
+        "smx_tune_shard_xchg": ([i32], ctypes.c_int),
         "smx_bshard_publish": ([sp, i32, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_host_select": ([vp, sp, vp], ctypes.c_int),
         "smx_host_pivot": ([vp, vp, sp, i32, i32], ctypes.c_int),
@@ -225,6 +230,13 @@ def tune_block_pipe(on: int = -1) -> int:
     default), 0 plan every block on the solver stream, -1 query only; returns the previous
     setting."""
     return int(load().smx_tune_block_pipe(on))
+
+
+def tune_shard_xchg(mode: int = -2) -> int:
+    """smx_tune_shard_xchg: -1 automatic (light from 4 ranks on), 0 full send slots, 1 light
+    (header all-gather + one max all-reduce of the pivot row), -2 query only; returns the previous
+    setting."""
+    return int(load().smx_tune_shard_xchg(mode))
 
 
 BLOCK_MAX = 16   # pivots per sweep at most (kBlkMax)

@@ -276,6 +276,30 @@ class BlockShardBackend:
             self._nbytes, d.log.data_ptr(), d.xhist.data_ptr(), d.log_cap,
             d.stream.cuda_stream), "smx_bshard_step")
 
+    # -- the light exchange: header all-gather, pick, max all-reduce of one row ----------------
+    @property
+    def row(self) -> torch.Tensor:
+        """The pivot-row buffer of the light exchange (after the gathered headers in recv)."""
+        h = self.world * _lib.SHARD_HDR
+        return self.recv[h:h + self.dev.ld]
+
+    def pick(self, rank: int) -> None:
+        """smx_bshard_pick: the owner of the winning row copies it into ``row``, the others
+        fill it with the bit pattern 0x8000000000000000 (a MAX all-reduce on int64 follows)."""
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_pick(
+            self.recv.data_ptr(), ctypes.byref(self._shape), self.world, rank,
+            self.send.data_ptr(), self.row.data_ptr(), d.stream.cuda_stream), "smx_bshard_pick")
+
+    def decide_light(self, step: int, pivots: int, parity: int, block: int) -> None:
+        """smx_bshard_step_light: decide from the gathered headers, pivot row from ``row``."""
+        d = self.dev
+        _lib.check(_lib.load().smx_bshard_step_light(
+            d.buf[parity].data_ptr(), ctypes.byref(self._shape), step, pivots, parity, block,
+            self.recv.data_ptr(), self.row.data_ptr(), self.world, d.ctl.data_ptr(),
+            self.blk.data_ptr(), self._nbytes, d.log.data_ptr(), d.xhist.data_ptr(), d.log_cap,
+            d.stream.cuda_stream), "smx_bshard_step_light")
+
     def sweep(self, pivots: int, parity: int) -> None:
         d = self.dev
         _lib.check(_lib.load().smx_bshard_sweep(
@@ -331,10 +355,15 @@ class BlockShardBackend:
         return self.dev.download()
 
 
-def run_block_protocol(be, k: int, exchange, pivots: int | None = None) -> None:
-    """k pivots of the block protocol on one rank's backend with any exchange (``exchange()``
-    all-gathers ``be.send`` into ``be.recv``): prime; per block of P pivots, P times pack ->
-    exchange -> step, then one sweep; publish.  Stream-ordered, no host synchronisation."""
+def run_block_protocol(be, k: int, exchange, pivots: int | None = None, reduce_row=None,
+                       rank: int | None = None) -> None:
+    """k pivots of the block protocol on one rank's backend with any exchange: prime; per block
+    of P pivots, P times pack -> exchange -> step, then one sweep; publish.  Full exchange
+    (``reduce_row`` None): ``exchange()`` all-gathers ``be.send`` into ``be.recv``.  Light
+    exchange: ``exchange()`` all-gathers the SHARD_HDR-double headers of ``be.send`` into the
+    start of ``be.recv``, ``be.pick(rank)`` fills ``be.row``, ``reduce_row()`` all-reduces it with
+    MAX over its int64 bit patterns, ``be.decide_light`` steps.  Stream-ordered, no host
+    synchronisation."""
     P = int(pivots if pivots is not None else be.pivots)
     with be.stream_ctx():
         be.prime()
@@ -345,7 +374,12 @@ def run_block_protocol(be, k: int, exchange, pivots: int | None = None) -> None:
             for step in range(1, pb + 1):
                 be.pack(step - 1, pb, bn, parity)
                 exchange()
-                be.decide(step, pb, parity, bn)
+                if reduce_row is None:
+                    be.decide(step, pb, parity, bn)
+                else:
+                    be.pick(rank)
+                    reduce_row()
+                    be.decide_light(step, pb, parity, bn)
             be.sweep(pb, parity)
             parity = (parity + pb) & 1
             done += pb
@@ -409,6 +443,9 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     local[-1, :m] = lp.objective(args.kind, args.seed, m)
     pivots = int(getattr(args, "pivots", 8) or 1)
     block = pivots > 1
+    xmode = {"auto": -1, "full": 0, "light": 1}[getattr(args, "xchg", "auto") or "auto"]
+    _lib.tune_shard_xchg(xmode)
+    light = block and (world >= 4 if xmode < 0 else xmode == 1)
     if block:
         be = BlockShardBackend(local, n, m, m, lo, world, device=device,
                                log_cap=max(1 << 16, args.warmup + args.steps), pivots=pivots)
@@ -452,6 +489,11 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     dist.all_reduce(mn, op=dist.ReduceOp.MIN)
     wall = float(mx[0])
     local_bytes = 16.0 * (hi - lo + 1) * C
+    ld = be.dev.ld
+    # bytes each rank receives per pivot: full = every rank's slot (8 + 2 ld doubles); light =
+    # the headers plus a ring all-reduce of one row (~2 (N - 1) / N rows)
+    xbytes = (8 * world * 8 + 2.0 * (world - 1) / world * ld * 8) if light else \
+        (world * (8 + 2 * ld) * 8)
     if rank == 0:
         avg_upd = float(upd_ms.mean()) * 1e-3
         achieved = local_bytes / avg_upd / 1e9
@@ -472,14 +514,16 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
             "data": "synthetic: seeded dense random LP, each rank generates its own row block "
                     "on the host and uploads it to its HBM before timing (no dataset)",
             "config": {"workload": workload, "rows": R, "cols": C, "n": n, "m": m,
-                       "parallelism": f"row-shard x{world} (1 RCCL all-gather per pivot, "
-                                      "issued natively on the solver stream)",
+                       "parallelism": f"row-shard x{world} (RCCL exchange per pivot, issued "
+                                      "natively on the solver stream)",
                        "rows_per_rank": hi - lo,
                        "pivots_per_sweep": pivots if block else 1,
                        "kernels_per_pivot": (2 * pivots + 1) / pivots if block
                        else (2 if be.fused else 3),
                        "gather_overlapped_with_sweep": False if block else be.overlap,
-                       "collectives_per_pivot": 1},
+                       "exchange": "light" if light else "full",
+                       "collectives_per_pivot": 2 if light else 1,
+                       "exchange_bytes_per_pivot_per_rank": xbytes},
             "equiv_one_pass_gbs": 16.0 * R * C / (wall / args.steps) / 1e9,
             "equiv_one_pass_note": "16 B/element/pivot of the whole tableau over wall time per "
                                    "pivot; not HBM traffic (block sweeps move 16 B/element once "

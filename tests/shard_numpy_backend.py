@@ -91,12 +91,9 @@ class NumpyShardBackend:
             send[HDR + self.ld:HDR + 2 * self.ld] = self.T[rb - self.row0]
 
     # -- k_merge + k_update<kShard> ---------------------------------------------------------
-    def finish(self, ev_before=None, ev_after=None):
-        p = self.step & 1
-        self.step += 1
-        if self.term:
-            return
-        recv = self.recv.numpy().reshape(self.world, self.slot)
+    def _merge(self, recv):
+        """merge_headers over recv = [world][stride] (headers first): (status, r, c, owner,
+        offset of the winning row in the owner's send slot)."""
         gnegb, owner_b, gfirst, owner_f, fv = NONE, -1, NONE, -1, 0.0
         best, owner_best, c = (3, NONE, 0.0), -1, NONE
         for q in range(self.world):
@@ -109,9 +106,9 @@ class NumpyShardBackend:
             if _better(o, best):
                 best, owner_best = o, q
             c = int(h[6])
-        r, row = NONE, None
+        r, owner, off = NONE, -1, 0
         if gnegb != NONE:
-            r, row = gnegb, recv[owner_b, HDR + self.ld:HDR + 2 * self.ld]
+            r, owner, off = gnegb, owner_b, HDR + self.ld
             c = int(recv[owner_b, 7])
             status = PIVOT if c != NONE else INCORRECT
         elif c == NONE:
@@ -119,11 +116,27 @@ class NumpyShardBackend:
         elif gfirst == NONE:
             status = NOT_CONVERGE
         elif np.isnan(fv):
-            status, r, row = PIVOT, gfirst, recv[owner_f, HDR:HDR + self.ld]
+            status, r, owner, off = PIVOT, gfirst, owner_f, HDR
         elif best[0] >= 2:
             status = NOT_CONVERGE
         else:
-            status, r, row = PIVOT, best[1], recv[owner_best, HDR + self.ld:HDR + 2 * self.ld]
+            status, r, owner, off = PIVOT, best[1], owner_best, HDR + self.ld
+        return status, r, c, owner, off
+
+    def finish(self, ev_before=None, ev_after=None):
+        recv = self.recv.numpy().reshape(self.world, self.slot)
+        self._apply(recv, None)
+
+    def _apply(self, recv, row):
+        """the pivot from the merged headers; row = the pivot row (light exchange) or None (it
+        is read from the gathered slots)"""
+        p = self.step & 1
+        self.step += 1
+        if self.term:
+            return
+        status, r, c, owner, off = self._merge(recv)
+        if status == PIVOT and row is None:
+            row = recv[owner, off:off + self.ld]
         self.status, self.r, self.c = status, r, c
         if status != PIVOT:
             self.term = True
@@ -183,6 +196,28 @@ class NumpyBlockShardBackend(NumpyShardBackend):
     def decide(self, step, pivots, parity, block):
         self.calls.append(("decide", step, pivots, block))
         self.finish()
+
+    # -- the light exchange (smx_bshard_pick / smx_bshard_step_light) --------------------------
+    @property
+    def row(self):
+        return self.recv[self.world * HDR:self.world * HDR + self.ld]
+
+    def pick(self, rank):
+        self.calls.append(("pick", rank))
+        if self.term:
+            return
+        hdrs = self.recv.numpy()[:self.world * HDR].reshape(self.world, HDR)
+        status, r, c, owner, off = self._merge(hdrs)
+        out = self.row.numpy().view(np.int64)
+        if status == PIVOT and owner == rank:
+            out[:] = self.send.numpy()[off:off + self.ld].view(np.int64)
+        else:
+            out[:] = np.iinfo(np.int64).min
+
+    def decide_light(self, step, pivots, parity, block):
+        self.calls.append(("decide", step, pivots, block))
+        hdrs = self.recv.numpy()[:self.world * HDR].reshape(self.world, HDR)
+        self._apply(hdrs, self.row.numpy().copy())
 
     def sweep(self, pivots, parity):
         self.calls.append(("sweep", pivots, parity))

@@ -35,9 +35,12 @@ def _backends(T, n, m, world, pivots):
     return bes
 
 
-def _lockstep(bes, k, P):
-    """run_block_protocol for every simulated rank at once (the exchange is a device copy)."""
+def _lockstep(bes, k, P, light=False):
+    """run_block_protocol for every simulated rank at once (the exchange is a device copy).
+    light: the headers are copied, every rank picks, and the pivot-row buffers are reduced with
+    MAX over their int64 bit patterns (what the RCCL all-reduce of the light exchange does)."""
     import torch
+    hdr = 8
     for be in bes:
         with be.stream_ctx():
             be.prime()
@@ -50,13 +53,30 @@ def _lockstep(bes, k, P):
                 with be.stream_ctx():
                     be.pack(step - 1, pb, bn, parity)
             torch.cuda.synchronize()
-            allsend = torch.cat([be.send for be in bes])
+            if not light:
+                allsend = torch.cat([be.send for be in bes])
+                for be in bes:
+                    be.recv.copy_(allsend)
+                torch.cuda.synchronize()
+                for be in bes:
+                    with be.stream_ctx():
+                        be.decide(step, pb, parity, bn)
+                continue
+            allhdr = torch.cat([be.send[:hdr] for be in bes])
             for be in bes:
-                be.recv.copy_(allsend)
+                be.recv[:len(bes) * hdr].copy_(allhdr)
+            torch.cuda.synchronize()
+            for q, be in enumerate(bes):
+                with be.stream_ctx():
+                    be.pick(q)
+            torch.cuda.synchronize()
+            rowmax = torch.stack([be.row.view(torch.int64) for be in bes]).amax(dim=0)
+            for be in bes:
+                be.row.view(torch.int64).copy_(rowmax)
             torch.cuda.synchronize()
             for be in bes:
                 with be.stream_ctx():
-                    be.decide(step, pb, parity, bn)
+                    be.decide_light(step, pb, parity, bn)
         for be in bes:
             with be.stream_ctx():
                 be.sweep(pb, parity)
@@ -89,13 +109,14 @@ def _result(bes):
     ("uniform", 4095, 4095, 2, 8, [24]),
     ("degenerate_mixed", 9, 3, 4, 2, [40]),
 ])
-def test_block_shards_match_oracle(kind, n, m, world, P, chunks):
+@pytest.mark.parametrize("light", [False, True])
+def test_block_shards_match_oracle(kind, n, m, world, P, chunks, light):
     from oracle import c_oracle
     from simplex_mi355x import lp
     T = lp.dense_tableau(kind, 7, n, m)
     bes = _backends(T, n, m, world, P)
     for chunk in chunks:
-        _lockstep(bes, chunk, P)
+        _lockstep(bes, chunk, P, light)
         if bes[0].state()["term"]:
             break
     states, logs, tables, full = _result(bes)
@@ -131,7 +152,7 @@ def test_block_shards_terminal_outcomes():
         Tref, st, done, log = c_oracle.run(T, n, m, m, 10_000, threads=4)
         world = 2 + seen % 2
         bes = _backends(T, n, m, world, 3 + seen % 4)
-        _lockstep(bes, done + 2, bes[0].pivots)
+        _lockstep(bes, done + 2, bes[0].pivots, light=bool(seen % 3 == 1))
         states, logs, tables, full = _result(bes)
         assert states[0]["npivots"] == done
         assert np.array_equal(logs[0], log)
@@ -141,12 +162,14 @@ def test_block_shards_terminal_outcomes():
     assert seen > 10
 
 
-def test_native_block_shard_chain_world1():
+@pytest.mark.parametrize("xchg", ["full", "light"])
+def test_native_block_shard_chain_world1(xchg):
     """bench.py --sharded at world size 1: smx_bshard_run_timed with libsmx's own RCCL
-    communicator, 8 pivots per sweep; the trajectory must stay valid."""
+    communicator, 8 pivots per sweep, both exchanges (light: header all-gather, pick, max
+    all-reduce on int64); the trajectory must stay valid."""
     env = dict(os.environ)
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--sharded",
-                          "--size", "2048", "--steps", "40", "--warmup", "8",
+                          "--size", "2048", "--steps", "40", "--warmup", "8", "--xchg", xchg,
                           "--no-cpu-baseline"], capture_output=True, text=True, env=env,
                          timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
@@ -154,3 +177,45 @@ def test_native_block_shard_chain_world1():
     d = json.loads(line)
     assert d["trajectory_valid"] and d["n_gpus"] == 1
     assert d["config"]["pivots_per_sweep"] == 8
+    assert d["config"]["exchange"] == xchg
+
+
+@pytest.mark.parametrize("light", [False, True])
+def test_block_shards_edge_fixtures(light):
+    """The edge fixtures (NaN first / later ratio candidates, inf, -0.0 "-b", m = 1, n = 1) on 2
+    and 3 simulated ranks, both exchanges: the NaN-first row travels as row A of its owner."""
+    from golden_util import dec_input, load
+    from oracle import c_oracle
+    seen = 0
+    for label, rec in load("edge.json").items():
+        cons, func = dec_input(rec["input"])
+        n, m = len(cons), len(cons[0]) - 1
+        if len(func) != m or m < 1:
+            continue
+        T = np.zeros((n + 1, m + 1))
+        T[:n] = np.array(cons, dtype=np.float64)
+        T[n, :m] = np.array(func, dtype=np.float64)
+        Tref, st, done, log = c_oracle.run(T, n, m, m, 200, threads=2)
+        for world in (2, 3):
+            bes = _backends(T, n, m, world, 3)
+            _lockstep(bes, min(done + 2, 200), 3, light)
+            states, logs, tables, full = _result(bes)
+            assert states[0]["npivots"] == done, label
+            assert np.array_equal(logs[0], log)
+            # NaN payloads / signs are not part of the contract (DESIGN.md section 1): NaN
+            # positions must agree, every other element bit for bit
+            a, b = full[:n], Tref[:n]
+            assert np.array_equal(np.isnan(a), np.isnan(b)), label
+            ok = ~np.isnan(a)
+            assert np.array_equal(a[ok].view(np.int64), b[ok].view(np.int64)), label
+        seen += 1
+    assert seen >= 5
+
+
+def test_native_block_shard_chain_both_exchanges_vs_oracle():
+    """smx_bshard_run with libsmx's own RCCL communicator at world size 1, full and light
+    exchange, against the C oracle (tools/check_native_bshard.py, its own process)."""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "check_native_bshard.py")],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, (out.stdout[-3000:], out.stderr[-3000:])
+    assert out.stdout.count(" ok") == 10, out.stdout

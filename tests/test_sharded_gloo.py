@@ -133,6 +133,7 @@ def _block_worker(rank, world, port, case, outdir):
     for p in (repo, os.path.join(repo, "simplex-method-solver_amd"), here):
         if p not in sys.path:
             sys.path.insert(0, p)
+    import torch
     import torch.distributed as dist
     from shard_numpy_backend import NumpyBlockShardBackend
     from simplex_mi355x.sharded import row_range, run_block_protocol
@@ -146,8 +147,18 @@ def _block_worker(rank, world, port, case, outdir):
     be = NumpyBlockShardBackend(local, n, m, m, lo, world, pivots=P)
     done = 0
     for chunk in case["chunks"]:
-        run_block_protocol(be, chunk, lambda: dist.all_gather_into_tensor(be.recv, be.send),
-                           pivots=P)
+        if case.get("light"):
+            # header all-gather, pick, MAX all-reduce of the pivot row's int64 bit patterns
+            hdr = 8
+            run_block_protocol(
+                be, chunk,
+                lambda: dist.all_gather_into_tensor(be.recv[:world * hdr], be.send[:hdr]),
+                pivots=P, rank=rank,
+                reduce_row=lambda: dist.all_reduce(be.row.view(torch.int64),
+                                                   op=dist.ReduceOp.MAX))
+        else:
+            run_block_protocol(be, chunk, lambda: dist.all_gather_into_tensor(be.recv, be.send),
+                               pivots=P)
         done += chunk
     st = be.state()
     gathered = [None] * world
@@ -162,17 +173,20 @@ def _block_worker(rank, world, port, case, outdir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("light", [False, True])
 @pytest.mark.parametrize("kind,n,m,world,P,chunks", [
     ("uniform", 64, 48, 2, 8, [20, 13]),
     ("mixed", 47, 33, 3, 3, [7, 30]),
     ("degenerate_mixed", 45, 25, 2, 5, [60]),
     ("mixed", 2, 6, 3, 4, [9, 9]),        # rank 0 owns no rows
 ])
-def test_block_protocol_matches_oracle(tmp_path, kind, n, m, world, P, chunks):
+def test_block_protocol_matches_oracle(tmp_path, kind, n, m, world, P, chunks, light):
+    """Both exchanges: the full send slots, and the light one (headers + the pivot row by a
+    MAX all-reduce over int64 bit patterns, -0.0 included)."""
     T = _case_T(kind, n, m, 3)
     np.save(tmp_path / "T.npy", T)
     k = sum(chunks)
-    case = {"n": n, "m": m, "k": k, "P": P, "chunks": chunks}
+    case = {"n": n, "m": m, "k": k, "P": P, "chunks": chunks, "light": light}
     mp.spawn(_block_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world,
              join=True)
     _compare(tmp_path, T, n, m, k)
@@ -185,7 +199,10 @@ def test_block_protocol_matches_oracle(tmp_path, kind, n, m, world, P, chunks):
         while done < chunk:
             pb = min(P, chunk - done)
             for step in range(1, pb + 1):
-                exp += [["pack", step - 1, pb, bn], ["decide", step, pb, bn]]
+                exp += [["pack", step - 1, pb, bn]]
+                if light:
+                    exp += [["pick", 0]]
+                exp += [["decide", step, pb, bn]]
             exp.append(["sweep", pb, None])
             done += pb
             bn += 1
