@@ -919,14 +919,14 @@ __device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, 
 // 1120-1184 us vs 1176-1293 us at P = 8), one vote for both.  Same values as blk_sweep_body.
 // Batch index (rows base + t*qs, batch t >> 1) of pivot q's row on this wave, lane q of the
 // wave holding it (0x7fffffff: another wave's row, or no pivot q)
-template <int P>
+template <int P, int ROWS = 2>
 __device__ __forceinline__ int blk_special_batch(const BlkHdr* __restrict__ h, int base, int qs) {
     const int q = threadIdx.x & (kWave - 1);
     int tb = 0x7fffffff;
     if (q < P) {
         const int rq = h->r[q];
         const int d = rq - base;
-        if (rq >= 0 && d >= 0 && d % qs == 0) tb = (d / qs) >> 1;
+        if (rq >= 0 && d >= 0 && d % qs == 0) tb = (d / qs) / ROWS;
     }
     return tb;
 }
@@ -1139,6 +1139,127 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no load in flight at exit
 }
 
+// The fixed-chunk sweep with ONE row per batch (two element chains per lane): half the per-row
+// multipliers live at a time (P instead of 2 P scalar registers), so large P does not spill
+// scalars into vector lanes inside the loop.  Next row's load issued before this row's
+// arithmetic (prefetch depth 1).  Same values as blk_sweep_body.
+template <int P, bool NTL>
+__device__ __forceinline__ void blk_sweep_body_row1(const double* Tin, double* Tout, int64_t ld,
+                                                    int R, int C, const BlkHdr* __restrict__ h,
+                                                    const double* __restrict__ pr,
+                                                    const double* __restrict__ mul) {
+    const int lane = threadIdx.x & (kWave - 1);
+    int rq[P], cq[P];
+    double eq[P], yq[P];
+    bool allok = true;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        rq[q] = h->r[q];
+        cq[q] = h->c[q];
+        eq[q] = h->e[q];
+        yq[q] = h->y[q];
+        allok = allok && h->ok[q] != 0;
+    }
+    constexpr int kChunk = 2 * kWave;
+    const int NW = (int)gridDim.x * kUpdWaves;
+    const int w = (int)blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunks = (C + kChunk - 1) / kChunk;
+    const int qs = NW / nchunks;
+    const int ch = w % nchunks;
+    const int j = ch * kChunk + 2 * lane;
+    const int c0 = ch * kChunk;
+    dbl2 prs[P];
+    bool colchunk = false;
+    uint32_t cbits = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
+                         : dbl2{0.0, 0.0};
+        colchunk = colchunk || (cq[q] >= c0 && cq[q] < c0 + kChunk);
+        cbits |= (cq[q] == j ? 1u : 0u) << (2 * q);
+        cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
+    }
+    const bool cspecial = !allok;
+    const int base = w / nchunks;
+    const int tbq = blk_special_batch<P, 1>(h, base, qs);
+    int tsp = blk_next_batch<P>(tbq, -1);
+    auto row1 = [&](dbl2 x0, int i0, int t) {
+        const double* m0 = mul + (int64_t)i0 * kBlkMax;
+        double pc0[P];
+        const bool special = cspecial || t == tsp;
+        if (t == tsp) tsp = blk_next_batch<P>(tbq, t);
+#pragma unroll
+        for (int q = 0; q < P; ++q) pc0[q] = m0[q];
+        dbl2 v0 = x0;
+        bool ok = false;
+        auto fast = [&](auto selc) {
+            constexpr bool SEL = decltype(selc)::value;
+            uint32_t wt = 0;
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const double e = eq[q], y = yq[q];
+                double n[2];
+                n[0] = v0[0] * e - prs[q][0] * pc0[q];
+                n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                if (SEL) {
+                    const bool s0 = (cbits >> (2 * q)) & 1u, s1 = (cbits >> (2 * q + 1)) & 1u;
+                    n[0] = s0 ? v0[0] : n[0];
+                    n[1] = s1 ? v0[1] : n[1];
+                }
+                double rr[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    wt = max(wt, win_term(n[k]));
+                    const double tq = n[k] * y;
+                    const double r = fma(-e, tq, n[k]);
+                    rr[k] = fma(r, y, tq);
+                }
+                v0 = dbl2{rr[0], rr[1]};
+            }
+            ok = __all(wt < kWinSpan);
+        };
+        if (!special) {
+            if (colchunk)
+                fast(SmxBool<true>{});
+            else
+                fast(SmxBool<false>{});
+        }
+        if (!ok) {
+            const int jl = min(j, (C - 1) & ~1);
+            x0 = *reinterpret_cast<const dbl2*>(Tin + (int64_t)i0 * ld + jl);
+            v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
+        }
+        if (j < C)
+            __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
+    };
+    // prefetch depth 1 over single rows: before a register set is used, the ops issued after
+    // its load are the previous row's store and the other set's load (vmcnt(2); vmcnt(1) first)
+    const int jc = min(j, (C - 1) & ~1);
+    auto ldc = [&](int row) {
+        dbl2 v;
+        const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
+        if (NTL)
+            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+        else
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+        return v;
+    };
+    dbl2 a = ldc(base), b = ldc(base + qs);
+    asm volatile("s_waitcnt vmcnt(1)" : "+v"(a) :: "memory");
+    int t = 0;
+    for (int i0 = base; i0 < R; i0 += 2 * qs, t += 2) {
+        row1(a, i0, t);
+        if (i0 + qs >= R) break;
+        a = ldc(i0 + 2 * qs);
+        asm volatile("s_waitcnt vmcnt(2)" : "+v"(b) :: "memory");
+        row1(b, i0 + qs, t + 1);
+        if (i0 + 2 * qs >= R) break;
+        b = ldc(i0 + 3 * qs);
+        asm volatile("s_waitcnt vmcnt(2)" : "+v"(a) :: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Output: in place when ipx >= 0 and ipx + (pivots applied) is even, else into b_other; the
 // chain state's loc records which buffer (in_idx = index of b_in) now holds the newest table.
 __device__ __forceinline__ double* blk_out(double* b_in, double* b_other, int ipx, int in_idx,
@@ -1163,7 +1284,9 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
                                                          int in_idx) {
     if (h->peff != P) return;
     double* out = blk_out(b_in, b_other, ipx, in_idx, P, hs);
-    if constexpr (FORM > 0)
+    if constexpr (FORM == 3)
+        blk_sweep_body_row1<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
+    else if constexpr (FORM > 0)
         blk_sweep_body_fixed<P, NTL, (P >= 7), FORM>(b_in, out, ld, R, C, h, pr, mul);
     else
         blk_sweep_body<P, NTL>(b_in, out, ld, R, C, h, pr, mul);

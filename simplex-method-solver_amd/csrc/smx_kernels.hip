@@ -459,6 +459,7 @@ BlkSweepFn blk_sweep_fn(int P, bool ntl, int form) {
     using All = std::make_integer_sequence<int, kBlkMax>;
     using Low = std::make_integer_sequence<int, 8>;
     if (ntl || P > 8) {
+        if (form == 3) return blk_sweep_pick<true, 3>(P, All{});
         if (form == 2) return blk_sweep_pick<true, 2>(P, All{});
         return form ? blk_sweep_pick<true, 1>(P, All{}) : blk_sweep_pick<true, 0>(P, All{});
     }
@@ -589,8 +590,17 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
         return e ? atoi(e) : 0;
     }();
     const int depth = depth_env == 2 ? 2 : 1;
+    // one row per batch from 10 pivots on (blk_sweep_body_row1: fewer scalar spills; 16384^2
+    // sweeps 1054 / 1260 / 1381 us at P = 10 / 12 / 14 vs 1078 / 1282 / 1389 with two rows,
+    // the same at 8: profiles/r02/sweep_rows_ab.jsonl).  SMX_BLK_ROWS (experiments): 1 or 2
+    // rows per batch for every P.
+    static const int rows_env = [] {
+        const char* e = getenv("SMX_BLK_ROWS");
+        return e ? atoi(e) : 0;
+    }();
+    const bool row1 = rows_env == 1 || (rows_env == 0 && P >= 10);
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    BlkSweepFn fn = blk_sweep_fn(P, ntl, P >= 7 ? depth : 1);
+    BlkSweepFn fn = blk_sweep_fn(P, ntl || row1, row1 ? 3 : (P >= 7 ? depth : 1));
     int grid = update_grid(s, (const void*)fn, 0, bpc_env);
     if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
         fn = blk_sweep_fn(P, ntl, 0);

@@ -1,10 +1,12 @@
 """The committed bench evidence keeps the driver's contract (CPU only: reads profiles/).
 
-profiles/r01_bench_default.json is the default `python bench.py` line of this round's GPU run;
-profiles/r01_block_16384_* are the rocprofv3 kernel-trace stats and PMC passes of the same
-command (tools/profile_round.sh).  The checks: the JSON line's keys and types, the roofline
-arithmetic (achieved = algorithmic bytes / average launch, frac = achieved / peak), the
-cpu_baseline block, and that the HIP-event launch average agrees with rocprofv3's.
+profiles/r02/bench_default.json is a `python bench.py --steps 20 --warmup 5` line (the driver's
+command) of this round's GPU run, with its cpu_baseline; profiles/r02/bench_steps200.json and
+kernel_stats_16384_steps200.csv are the bench line and rocprofv3 kernel-trace stats of the same
+command (tools/profile_r02.sh), profiles/r02/pmc/ its FETCH_SIZE / WRITE_SIZE passes.  The
+checks: the JSON line's keys and types, the roofline arithmetic (achieved = algorithmic bytes /
+average launch, frac = achieved / peak), the cpu_baseline block, and that the HIP-event launch
+average agrees with rocprofv3's.
 """
 import csv
 import json
@@ -33,7 +35,7 @@ def _rocprof_avg_ms(name, needle):
 
 
 def test_default_line_keys():
-    rec = _line("r01_bench_default.json")
+    rec = _line("r02/bench_default.json")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
               "roofline", "cpu_baseline"):
@@ -46,7 +48,7 @@ def test_default_line_keys():
 
 
 def test_roofline_arithmetic():
-    r = _line("r01_bench_default.json")["roofline"]
+    r = _line("r02/bench_default.json")["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     ach = r["algorithmic_bytes_per_launch"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
     assert r["achieved"] == pytest.approx(ach, rel=1e-9)
@@ -58,22 +60,22 @@ def test_roofline_arithmetic():
 
 
 def test_cpu_baseline_block():
-    cb = _line("r01_bench_default.json")["cpu_baseline"]
+    cb = _line("r02/bench_default.json")["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1
     assert cb["value"] > 0 and cb["unit"] == "pivots/s" and cb["sample"]
 
 
 def test_event_average_agrees_with_rocprof():
-    rec = _line("r01_block_16384_bench.log")
+    rec = _line("r02/bench_steps200.json")
     r = rec["roofline"]
-    prof = _rocprof_avg_ms("r01_block_16384_kernel_stats.csv", "k_blk_sweep<8")
-    assert r["kernel"] == "k_blk_sweep<8>"
+    prof = _rocprof_avg_ms("r02/kernel_stats_16384_steps200.csv", "k_blk_sweep<")
+    assert r["kernel"] == "k_blk_sweep<12>"
     assert abs(r["avg_kernel_ms"] - prof) / prof < 0.10, (r["avg_kernel_ms"], prof)
 
 
 def test_pmc_summary_matches_csv_passes():
     with open(os.path.join(PROF, "pmc_traffic.json")) as fh:
-        t = json.load(fh)["16384x16384/k_blk_sweep<8>"]
+        t = json.load(fh)["16384x16384/k_blk_sweep<12>"]
     assert t["bytes_per_launch"] == pytest.approx(t["read_bytes_corrected"] + t["write_bytes"])
     assert t["read_bytes_corrected"] == pytest.approx(2 * 1024 * t["fetch_size_kib_median"])
     assert t["write_bytes"] == pytest.approx(1024 * t["write_size_kib_median"])
