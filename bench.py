@@ -59,9 +59,10 @@ def parse():
     ap.add_argument("--traffic", default=None, help="PMC summary json (default: profiles/)")
     ap.add_argument("--sharded", action="store_true",
                     help="use the row-sharded RCCL path even at world size 1")
-    ap.add_argument("--pivots", type=int, default=8,
-                    help="row-sharded path: pivots per sweep (block pivots; 1 = one pivot per "
-                         "sweep, the fused one-pivot protocol)")
+    ap.add_argument("--pivots", type=int, default=None,
+                    help="row-sharded path: pivots per sweep at most (block pivots; 1 = one "
+                         "pivot per sweep, the fused one-pivot protocol; default: 12 / 10 / 8 by "
+                         "the size of each rank's table, as the single-GPU policy)")
     ap.add_argument("--xchg", choices=("auto", "full", "light"), default="auto",
                     help="row-sharded block path: exchange per pivot (full = all-gather of every "
                          "rank's header + 2 candidate rows; light = header all-gather + one "

@@ -107,7 +107,50 @@ inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
 struct BlkPiv {
     int r[kBlkMax], c[kBlkMax];
     double e[kBlkMax];
+    double y[kBlkMax];   // refined reciprocal of e (fd_prep; register copies only, blk_pv_regs)
 };
+
+constexpr double kFdMinAbs = 0x1p-127;   // biased exponent 896
+constexpr double kFdMaxAbs = 0x1p130;    // biased exponent 1152 is the last inside
+// The same window on the high dword with 32-bit integer ops: t = (hi << 1) + kWinBias (mod 2^32)
+// drops the sign and is < kWinSpan exactly when the biased exponent lies in [896, 1152] (fd_in);
+// NaN, infinities, zeros and denormals fall outside.  A running unsigned max per lane replaces
+// the two fp64 min/max per element and pivot (tools/sweep_probe.hip, profiles/r02_sweep_probe*).
+constexpr uint32_t kWinBias = 0x90000000u;   // -(896 << 21) mod 2^32
+constexpr uint32_t kWinSpan = 0x20200000u;   // (1153 - 896) << 21
+__device__ __forceinline__ uint32_t win_term(double n) {
+    uint32_t t;
+    // one v_lshl_add_u32 (written out: the compiler turns the shift of the high dword into an
+    // alignbit + and + add sequence)
+    asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(t) : "v"(__double2hiint(n)), "s"(kWinBias));
+    return t;
+}
+
+
+// chain() with the division in its hoisted-reciprocal form (3 dependent fp64 ops instead of the
+// ~10 of the IEEE sequence): bit-identical while every numerator stays inside the window, which
+// `wt` tracks (win_term; a caller recomputes with blk_chain when a wave vote says otherwise,
+// or when a pivot element itself is outside the window).  The planner's chains are latency-
+// bound -- one wave per SIMD, steps in sequence -- so this is what shortens them.
+template <int L>
+__device__ __forceinline__ double blk_chain_fd(double x, int i, int j, const BlkPiv& pv,
+                                               const double* p, const double* mq, uint32_t& wt) {
+#pragma unroll
+    for (int q = 0; q < L; ++q) {
+        const double e = pv.e[q];
+        // branch-free (the row and column tests differ across lanes): both numerators, then
+        // a select -- the pivot row's products are computed and discarded
+        const double a = x * e;
+        const double b = p[q] * mq[q];
+        const bool jc = j == pv.c[q];
+        const double num = (i == pv.r[q]) ? (jc ? 1.0 : -x) : (jc ? x : (a - b));
+        wt = max(wt, win_term(num));
+        const double t = num * pv.y[q];
+        const double r = fma(-e, t, num);
+        x = fma(r, pv.y[q], t);
+    }
+    return x;
+}
 
 // T_{k+L}[i][j] from x = T_k[i][j]; p[q] = pr_q[j], mq[q] = mul[i][q] (loaded by the caller, all
 // before the first use, so a chain costs one memory round trip, not L)
@@ -117,14 +160,12 @@ __device__ __forceinline__ double blk_chain(double x, int i, int j, const BlkPiv
 #pragma unroll
     for (int q = 0; q < L; ++q) {
         const double e = pv.e[q];
-        double num;
-        if (i == pv.r[q]) {
-            num = (j == pv.c[q]) ? 1.0 : -x;
-        } else {
-            const double a = x * e;
-            const double b = p[q] * mq[q];
-            num = (j == pv.c[q]) ? x : (a - b);
-        }
+        // branch-free (the row and column tests differ across lanes): both numerators, then
+        // a select -- the pivot row's products are computed and discarded
+        const double a = x * e;
+        const double b = p[q] * mq[q];
+        const bool jc = j == pv.c[q];
+        const double num = (i == pv.r[q]) ? (jc ? 1.0 : -x) : (jc ? x : (a - b));
         x = num / e;
     }
     return x;
@@ -144,24 +185,59 @@ __device__ __forceinline__ double blk_chain_rolled(double x, int i, int j, const
 #pragma unroll 1
     for (int q = 0; q < n; ++q) {
         const double e = pv.e[q];
-        double num;
-        if (i == pv.r[q]) {
-            num = (j == pv.c[q]) ? 1.0 : -x;
-        } else {
-            const double a = x * e;
-            const double b = p[q] * mq[q];
-            num = (j == pv.c[q]) ? x : (a - b);
-        }
+        // branch-free (the row and column tests differ across lanes): both numerators, then
+        // a select -- the pivot row's products are computed and discarded
+        const double a = x * e;
+        const double b = p[q] * mq[q];
+        const bool jc = j == pv.c[q];
+        const double num = (i == pv.r[q]) ? (jc ? 1.0 : -x) : (jc ? x : (a - b));
         x = num / e;
     }
     return x;
 }
+
+// A chain's operands must all be in registers before its first step: left to itself the
+// compiler sinks each load next to its use, and a chain of L steps then waits for L memory round
+// trips one after the other (the planner's scans and row pass grew by ~0.5 us per chain step,
+// tools/trace_planner.hip).  An empty asm that "modifies" a value forces its load to have landed
+// there, so all of a chain's loads are issued together and waited for once.
+__device__ __forceinline__ void blk_pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void blk_pin(int& x) { asm volatile("" : "+v"(x)); }
 
 template <int L>
 __device__ __forceinline__ void blk_load_col(const double* __restrict__ pr, int64_t ld, int j,
                                              double* p) {
 #pragma unroll
     for (int q = 0; q < L; ++q) p[q] = pr[(int64_t)q * ld + j];
+#pragma unroll
+    for (int q = 0; q < L; ++q) blk_pin(p[q]);
+}
+
+// The first L pivots of an LDS-broadcast BlkPiv in registers (see blk_pin)
+template <int L>
+__device__ __forceinline__ BlkPiv blk_pv_regs(const BlkPiv& s, bool* allok = nullptr) {
+    BlkPiv v;
+#pragma unroll
+    for (int q = 0; q < L; ++q) {
+        v.r[q] = s.r[q];
+        v.c[q] = s.c[q];
+        v.e[q] = s.e[q];
+    }
+#pragma unroll
+    for (int q = 0; q < L; ++q) {
+        blk_pin(v.r[q]);
+        blk_pin(v.c[q]);
+        blk_pin(v.e[q]);
+    }
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < L; ++q) {
+        const FastDiv f = fd_prep(v.e[q]);
+        v.y[q] = f.y;
+        ok = ok && f.ok;
+    }
+    if (allok) *allok = ok;
+    return v;
 }
 
 // Row r of T_{k+D} at column j (the pivot row of block step D; mqr = mul[r][0..D))
@@ -406,6 +482,24 @@ __global__ __launch_bounds__(kUpdBlock) void k_bsh_pick(const double* __restrict
         out[j] = own ? (unsigned long long)__double_as_longlong(src[j]) : 0x8000000000000000ull;
 }
 
+#ifdef SMX_BLK_TRACE
+// Diagnostic build only (tools/trace_planner.hip): per-workgroup s_memrealtime stamps (100 MHz,
+// chip-wide) of every planner step, [block step L][workgroup][phase]: 0 entry, 1 decision known,
+// 2 pivot element known, 3 pivot-row / f-row slice written, 4 next entering column found,
+// 5 row pass operands staged, 6 row pass done, 7 records stored.
+constexpr int kBlkTraceParts = 64;
+__device__ unsigned long long g_blk_trace[kBlkMax + 1][kBlkTraceParts][8];
+#define SMX_BLK_STAMP(ph)                                                              \
+    do {                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < kBlkTraceParts)                           \
+            g_blk_trace[L][blockIdx.x][ph] = __builtin_amdgcn_s_memrealtime();         \
+    } while (0)
+#else
+#define SMX_BLK_STAMP(ph) \
+    do {                  \
+    } while (0)
+#endif
+
 // One pivot of the block: decide block step D = L-1 and build the records of step L.
 // SH = false: the decision from the records of step D and the pivot-row values derived on the
 // fly; SH = true (row-sharded): from the P gathered send slots in `recv` (merge_headers), the
@@ -446,6 +540,7 @@ __device__ __forceinline__ bool blk_step_body(
     __shared__ double s_e, s_fc, s_pm, s_pa;
     const int tid = threadIdx.x;
     const int b = blockIdx.x, G = gridDim.x;
+    SMX_BLK_STAMP(0);
     if (!LAG) pp = 0;
     if (ctl->term) {
         if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
@@ -517,6 +612,7 @@ __device__ __forceinline__ bool blk_step_body(
         }
     }
     __syncthreads();
+    SMX_BLK_STAMP(1);
     const int nb = s_nb;
     Decision d = s_d;
     auto terminal = [&](const Decision& dd) {
@@ -546,7 +642,12 @@ __device__ __forceinline__ bool blk_step_body(
     } else if (!SH) {
 #pragma unroll
         for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)r_local * kBlkMax + q];
+#pragma unroll
+        for (int q = 0; q < D; ++q) blk_pin(mqr[q]);
     }
+    // this block's first D pivots in registers (s_pv is complete up to D since the decision)
+    bool okD = true;
+    const BlkPiv pvD = blk_pv_regs<D>(s_pv, &okD);
     auto prv = [&](int j) -> double {
         if (SH) return prow[j];
         if constexpr (LAG) {
@@ -559,9 +660,14 @@ __device__ __forceinline__ bool blk_step_body(
             return blk_chain_rolled(T[(int64_t)r_local * ld + j], r_local, j, s_all, pp + D, op,
                                     s_mrall);
         }
+        double x = T[(int64_t)r_local * ld + j];
         double p[kBlkMax];
         blk_load_col<D>(pr, ld, j, p);
-        return blk_chain<D>(T[(int64_t)r_local * ld + j], r_local, j, s_pv, p, mqr);
+        blk_pin(x);
+        uint32_t wt = 0;
+        const double v = blk_chain_fd<D>(x, r_local, j, pvD, p, mqr, wt);
+        if (okD && __all(wt < kWinSpan)) return v;
+        return blk_chain<D>(x, r_local, j, pvD, p, mqr);
     };
     const double* fo = fr + (int64_t)sp * ld;          // f-row of T_{k+D}
     double* fn = fr + (int64_t)(sp ^ 1) * ld;          // f-row of T_{k+L}
@@ -594,6 +700,7 @@ __device__ __forceinline__ bool blk_step_body(
         s_pm = prv(m);
     }
     __syncthreads();
+    SMX_BLK_STAMP(2);
     const double e = s_e, fc = s_fc;
     // slice b of the pivot row and of the next f-row
     {
@@ -605,6 +712,7 @@ __device__ __forceinline__ bool blk_step_body(
             fn[j] = blk_fnew(fo[j], v, j, c, e, fc);
         }
     }
+    SMX_BLK_STAMP(3);
     // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
     int cf = SMX_NONE;
     for (int j0 = 0; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
@@ -616,6 +724,7 @@ __device__ __forceinline__ bool blk_step_body(
         }
         cf = block_min_int<NT>(mine, s_tmp);
     }
+    SMX_BLK_STAMP(4);
     if (tid == 0) s_pa = cf != SMX_NONE ? prv(cf) : 0.0;
     // the labels after this pivot (simplex.py:152), identically in every workgroup
     const int hx0 = move_label(ctl->xpos[sp][0], r, c);
@@ -685,6 +794,7 @@ __device__ __forceinline__ bool blk_step_body(
         }
     }
     __syncthreads();
+    SMX_BLK_STAMP(5);
     const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
     // x-history of this pivot: the labels' rows as local indices (their "-b" entries of T_{k+L})
     const int hl0 = hx0 >= row0 && hx0 < row0 + rows ? hx0 - row0 : -1;
@@ -695,6 +805,20 @@ __device__ __forceinline__ bool blk_step_body(
     // once (step 0) and the column the next step's records are built on -- the next entering
     // column in phase 2 -- is kept from the step that read it: one strided column per step
     // instead of three.
+    // the row pass's shared operands in registers: the L pivots and the pivot rows at c, m, cf
+    BlkPiv pvL;
+    bool okL = true;
+    double colv[3][kBlkMax];
+    if constexpr (!LAG) {
+        pvL = blk_pv_regs<L>(s_pv, &okL);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int q = 0; q < L; ++q) colv[k][q] = s_col[k][q];
+#pragma unroll
+            for (int q = 0; q < L; ++q) blk_pin(colv[k][q]);
+        }
+    }
     double* colm = fr + 2 * ld;
     double* colc = colm + rows;
     const bool reuse_c = D > 0 && c == s_c;   // phase 2: c is the column of step D's records
@@ -725,12 +849,23 @@ __device__ __forceinline__ bool blk_step_body(
             a = cf != SMX_NONE ? blk_chain_rolled(xa, i, cf, s_all, n + 1, s_colall[2], op) : 0.0;
         } else {
             double mq[kBlkMax];
+            double x3[3] = {xc, xb, xa};
 #pragma unroll
             for (int q = 0; q < D; ++q) mq[q] = mr[q];
-            mq[D] = blk_chain<D>(xc, i, c, s_pv, s_col[0], mq);   // T_{k+D}[i][c]
+#pragma unroll
+            for (int q = 0; q < D; ++q) blk_pin(mq[q]);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) blk_pin(x3[k]);
+            uint32_t wt = 0;
+            mq[D] = blk_chain_fd<D>(x3[0], i, c, pvL, colv[0], mq, wt);   // T_{k+D}[i][c]
+            bv = blk_chain_fd<L>(x3[1], i, m, pvL, colv[1], mq, wt);
+            a = cf != SMX_NONE ? blk_chain_fd<L>(x3[2], i, cf, pvL, colv[2], mq, wt) : 0.0;
+            if (!okL || !__all(wt < kWinSpan)) {   // some numerator outside the window
+                mq[D] = blk_chain<D>(x3[0], i, c, pvL, colv[0], mq);
+                bv = blk_chain<L>(x3[1], i, m, pvL, colv[1], mq);
+                a = cf != SMX_NONE ? blk_chain<L>(x3[2], i, cf, pvL, colv[2], mq) : 0.0;
+            }
             mr[D] = mq[D];
-            bv = blk_chain<L>(xb, i, m, s_pv, s_col[1], mq);
-            a = cf != SMX_NONE ? blk_chain<L>(xa, i, cf, s_pv, s_col[2], mq) : 0.0;
         }
         if (xhist && log_cap > 0) {
             if (i == hl0) xhist[hslot] = bv;
@@ -738,7 +873,9 @@ __device__ __forceinline__ bool blk_step_body(
         }
         blk_rec_add(R, row0 + i, bv, cf != SMX_NONE, a);
     }
+    SMX_BLK_STAMP(6);
     blk_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);
+    SMX_BLK_STAMP(7);
     return false;
 }
 
@@ -775,22 +912,6 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step_lag(SMX_BLK_STEP_PARAMS) {
 // holds no pivot column: numerators in the window form, with the smallest and largest |num| of
 // the whole chain tracked per lane; ONE wave vote per unit checks them against the window (and
 // the result against NaN) and otherwise the unit is recomputed with the hardware division.
-constexpr double kFdMinAbs = 0x1p-127;   // biased exponent 896
-constexpr double kFdMaxAbs = 0x1p130;    // biased exponent 1152 is the last inside
-// The same window on the high dword with 32-bit integer ops: t = (hi << 1) + kWinBias (mod 2^32)
-// drops the sign and is < kWinSpan exactly when the biased exponent lies in [896, 1152] (fd_in);
-// NaN, infinities, zeros and denormals fall outside.  A running unsigned max per lane replaces
-// the two fp64 min/max per element and pivot (tools/sweep_probe.hip, profiles/r02_sweep_probe*).
-constexpr uint32_t kWinBias = 0x90000000u;   // -(896 << 21) mod 2^32
-constexpr uint32_t kWinSpan = 0x20200000u;   // (1153 - 896) << 21
-__device__ __forceinline__ uint32_t win_term(double n) {
-    uint32_t t;
-    // one v_lshl_add_u32 (written out: the compiler turns the shift of the high dword into an
-    // alignbit + and + add sequence)
-    asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(t) : "v"(__double2hiint(n)), "s"(kWinBias));
-    return t;
-}
-
 template <int P>
 __device__ __forceinline__ dbl2 blk_exact(dbl2 v, int row, int j, const int* rq, const int* cq,
                                           const double* eq, const dbl2* prs, const double* pc) {

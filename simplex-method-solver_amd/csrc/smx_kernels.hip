@@ -638,9 +638,10 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, parity, ctl, bp, st);
     int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
-        // unsharded: balanced blocks; row-sharded: blocks of P and a ragged last one (the layout
-        // the step-wise smx_bshard_* protocol and its drivers use)
-        const int Pb = !sh ? block_size(k, P, bn) : ((k - done < P) ? k - done : P);
+        // blocks of near-equal size (every rank of a sharded chain cuts k the same way; the
+        // step-wise smx_bshard_* drivers may cut it differently -- the results do not depend on
+        // the cut)
+        const int Pb = block_size(k, P, bn);
         double* tin = p ? buf1 : buf0;
         double* toth = p ? buf0 : buf1;
         for (int l = 1; l <= Pb && !err; ++l) {
@@ -1702,7 +1703,7 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
     }
     int p = parity & 1, done = 0, bn = 0;
     while (!err && done < k) {
-        const int Pb = (k - done < pivots) ? k - done : pivots;
+        const int Pb = block_size(k, pivots, bn);
         for (int l = 1; l <= Pb && !err; ++l) {
             for (int q = 0; q < nranks && !err; ++q)
                 err = launch_bsh_pack(l - 1, buf(q, p), ranks[q].shape, Pb, bn, ranks[q].ctl,

@@ -441,7 +441,14 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     local = np.zeros((hi - lo + 1, m + 1), dtype=np.float64)
     local[:-1] = lp.dense_rows(args.kind, args.seed, n, m, lo, hi)
     local[-1, :m] = lp.objective(args.kind, args.seed, m)
-    pivots = int(getattr(args, "pivots", 8) or 1)
+    pivots = getattr(args, "pivots", None)
+    if pivots is None:
+        # the unsharded policy on the rank's own table: 12 pivots per sweep from 1 GiB, 10 from
+        # 256 MiB, else 8 (a sweep of 8 costs little more than one of 2 once the table is big)
+        ld = -(-(m + 1) // 16) * 16
+        rank_bytes = (hi - lo + 1) * ld * 8
+        pivots = 12 if rank_bytes >= (1 << 30) else (10 if rank_bytes >= (256 << 20) else 8)
+    pivots = int(pivots or 1)
     block = pivots > 1
     xmode = {"auto": -1, "full": 0, "light": 1}[getattr(args, "xchg", "auto") or "auto"]
     _lib.tune_shard_xchg(xmode)
@@ -449,6 +456,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     if block:
         be = BlockShardBackend(local, n, m, m, lo, world, device=device,
                                log_cap=max(1 << 16, args.warmup + args.steps), pivots=pivots)
+        nsw = -(-args.steps // pivots)    # blocks of near-equal size (block_size in libsmx)
     else:
         be = HipShardBackend(local, n, m, m, lo, world, device=device,
                              log_cap=max(1 << 16, args.warmup + args.steps))
@@ -518,7 +526,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
                                       "natively on the solver stream)",
                        "rows_per_rank": hi - lo,
                        "pivots_per_sweep": pivots if block else 1,
-                       "kernels_per_pivot": (2 * pivots + 1) / pivots if block
+                       "kernels_per_pivot": (2 * args.steps + nsw) / args.steps if block
                        else (2 if be.fused else 3),
                        "gather_overlapped_with_sweep": False if block else be.overlap,
                        "exchange": "light" if light else "full",
@@ -530,10 +538,10 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
                                    "per P pivots, spread over the ranks)",
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak_gbs, "unit": "GB/s",
                          "frac": achieved / peak_gbs, "traffic": traffic,
-                         "kernel": (f"k_blk_sweep<{pivots}>" if block else
+                         "kernel": (f"k_blk_sweep<{-(-args.steps // nsw)}>" if block else
                                     ("k_update<kShardFused>" if be.fused else "k_update<kShard>"))
                                    + " (rank 0)",
-                         "pivots_per_launch": pivots if block else 1,
+                         "pivots_per_launch": args.steps / nsw if block else 1,
                          "algorithmic_bytes_per_launch": local_bytes,
                          "avg_kernel_ms": avg_upd * 1e3,
                          "max_rank_avg_kernel_ms": float(mx[1]),
