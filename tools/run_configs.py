@@ -3,7 +3,8 @@
             fused chain, one hipGraph replay), plus a forced-pivot microbench (fixed r, c: the
             update alone, rule cost excluded).
   config 3: 8192x8192, seeds 0..2, K = 200.
-Each line: pivots/s, device us per pivot (HIP events around the replay / K), GB/s = 16 R C / that,
+Each line: pivots/s, device us per pivot (HIP events around the replay / K), equiv_one_pass_gbs =
+16 R C / that (not HBM traffic once a sweep carries several pivots: block pivots, resident loop),
 and whether the K pivots ran without reaching a terminal outcome.
 usage: python tools/run_configs.py [2,3] > out.jsonl"""
 import json
@@ -41,7 +42,7 @@ def chain(size, seed, k, warm):
     dev_us = e0.elapsed_time(e1) * 1e3 / max(done, 1)
     rec = {"size": size, "seed": seed, "K": k, "pivots": done, "terminal": bool(st["term"]),
            "pivots_per_s": done / wall, "device_us_per_pivot": dev_us,
-           "gbs": 16.0 * size * size / (dev_us * 1e-6) / 1e9}
+           "equiv_one_pass_gbs": 16.0 * size * size / (dev_us * 1e-6) / 1e9}
     dev.close()
     return rec
 
@@ -70,7 +71,7 @@ def forced(size, iters=200):
     del g
     dev.close()
     return {"size": size, "forced_update_us": us,
-            "gbs": 16.0 * size * size / (us * 1e-6) / 1e9,
+            "equiv_one_pass_gbs": 16.0 * size * size / (us * 1e-6) / 1e9,
             "note": "fixed (r, c) = (1, 2), graph replay, rule cost excluded"}
 
 
