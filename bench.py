@@ -42,6 +42,7 @@ for _p in (REPO, os.path.join(REPO, "simplex-method-solver_amd")):
 
 METRIC = "pivots/sec + achieved HBM GB/s, dense fp64 tableau, 1/2/4/8 MI355X"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -82,6 +83,33 @@ def load_traffic(path, workload):
         return None if rec is None else float(rec["bytes_per_launch"])
     except Exception:
         return None
+
+
+def load_valu(workload):
+    """VALU lane-instructions per element-pivot of a block sweep, from SQ_INSTS_VALU
+    (profiles/valu_instr.json, written by tools/valu_instr.py from the committed counter passes)."""
+    path = os.path.join(REPO, "profiles", "valu_instr.json")
+    try:
+        with open(path) as fh:
+            return float(json.load(fh)[workload]["instr_per_element_pivot"])
+    except Exception:
+        return None
+
+
+def two_term(R, C, pivots_per_launch, instr, avg_kernel, hbm_bytes):
+    """The sweep's two-term bound: fp64 VALU issue (one wave64 instruction per
+    CU per clock, 256 CUs at the 2.4 GHz peak clock) against HBM (8 TB/s); frac = the larger
+    term over the measured average sweep."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    wave_instr = R * C * pivots_per_launch * instr / 64.0
+    t_valu = wave_instr / (cus * PEAK_CLOCK_HZ)
+    t_hbm = hbm_bytes / (PEAK_HBM_GBS * 1e9)
+    return {"instr_per_element_pivot": instr, "wave_instr_per_launch": wave_instr,
+            "valu_peak_ms": t_valu * 1e3, "hbm_peak_ms": t_hbm * 1e3,
+            "bound": "valu" if t_valu > t_hbm else "hbm",
+            "frac": max(t_valu, t_hbm) / avg_kernel,
+            "valu_frac": t_valu / avg_kernel, "cus": cus, "peak_clock_ghz": PEAK_CLOCK_HZ / 1e9,
+            "source": "SQ_INSTS_VALU passes, profiles/valu_instr.json"}
 
 
 def shape_of(args):
@@ -257,10 +285,14 @@ def run_single(args):
         avg_kernel = float(np.mean(sw)) * 1e-3
         kernel = f"k_blk_sweep<{P_top}>"
         traffic = load_traffic(args.traffic, f"{R}x{C}/k_blk_sweep<{P_top}>")
+        instr = load_valu(f"{R}x{C}/{kernel}")
         extra = {"pivots_per_launch": args.steps / len(sw), "max_pivots_per_launch": P,
                  "launches": len(sw),
                  "planner_ms_per_pivot": (tot_ms - float(np.sum(sw))) / args.steps,
                  "algorithmic_bytes_per_pivot": bytes_per_sweep * len(sw) / args.steps}
+        if instr is not None:
+            extra["two_term"] = two_term(R, C, args.steps / len(sw), instr, avg_kernel,
+                                         bytes_per_sweep)
         kernels_per_pivot = (args.steps + len(sw)) / args.steps
     else:
         # the timed region replays one pre-captured hipGraph of K chained pivots (one fused

@@ -79,3 +79,21 @@ def test_pmc_summary_matches_csv_passes():
     assert t["bytes_per_launch"] == pytest.approx(t["read_bytes_corrected"] + t["write_bytes"])
     assert t["read_bytes_corrected"] == pytest.approx(2 * 1024 * t["fetch_size_kib_median"])
     assert t["write_bytes"] == pytest.approx(1024 * t["write_size_kib_median"])
+
+
+def test_valu_table_matches_counter_summaries():
+    """profiles/valu_instr.json (bench.py's two-term bound) is tools/valu_instr.py over the
+    committed SQ_INSTS_VALU summaries: lane-instructions per element-pivot of the sweep."""
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "valu_instr.py")],
+                         check=True, capture_output=True, text=True).stdout
+    with open(os.path.join(PROF, "valu_instr.json")) as fh:
+        committed = json.load(fh)
+    assert json.loads(out) == committed
+    for key, rec in committed.items():
+        assert key.startswith("16384x16384/k_blk_sweep<")
+        # ~3 f64 ops per element-pivot (a FMA-shaped update plus the exact rounding fix-ups) and
+        # the loads/stores/index arithmetic around them
+        assert 6.0 < rec["instr_per_element_pivot"] < 12.0
+        assert rec["f64_fma_mul_add_share"] > 0.6
