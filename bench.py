@@ -194,6 +194,16 @@ def cpu_baseline(T, n, m, seconds):
                          "cores": 1, "kind": "port",
                          "sample": f"{k} pivots (pick + pivot with deepcopy) at 1024x1024: "
                                    f"{ns_el:.0f} ns/element, scaled to {n + 1}x{m + 1}"}
+        # the restatement is faster per element than the reference itself (hoisted row reads):
+        # the ratio measured beside the reference in the build container (tools/cpu_rate_check.py)
+        try:
+            with open(os.path.join(REPO, "profiles", "r02", "cpu_rate_check.json")) as fh:
+                ratio = {r["size"]: r["ratio_restated_over_reference"]
+                         for r in json.load(fh)["rows"]}[1024]
+            out["python"]["restated_over_reference_ns"] = ratio
+            out["python"]["reference_estimate"] = out["python"]["value"] * ratio
+        except (OSError, KeyError, ValueError):
+            pass
     return out
 
 
