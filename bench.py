@@ -100,6 +100,7 @@ def two_term(R, C, pivots_per_launch, instr, avg_kernel, hbm_bytes):
     """The sweep's two-term bound: fp64 VALU issue (one wave64 instruction per
     CU per clock, 256 CUs at the 2.4 GHz peak clock) against HBM (8 TB/s); frac = the larger
     term over the measured average sweep."""
+    import torch
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     wave_instr = R * C * pivots_per_launch * instr / 64.0
     t_valu = wave_instr / (cus * PEAK_CLOCK_HZ)

@@ -601,7 +601,11 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     const bool row1 = rows_env == 1 || (rows_env == 0 && P >= 10);
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
     BlkSweepFn fn = blk_sweep_fn(P, ntl || row1, row1 ? 3 : (P >= 7 ? depth : 1));
-    int grid = update_grid(s, (const void*)fn, 0, bpc_env);
+    // the one-row form at P = 10..12 (72-83 VGPRs): 7 blocks per CU, above the occupancy API's
+    // 6 / 5 -- 1030-1044 vs 1070-1075 us per 10-pivot sweep and 1189-1196 vs 1234-1255 per
+    // 12-pivot sweep at 16384^2 (profiles/r02/sweep_bpc_row1_ab.jsonl; 8 is no better)
+    const int bpc_sweep = bpc_env > 0 ? bpc_env : (row1 && P <= 12 ? 7 : 0);
+    int grid = update_grid(s, (const void*)fn, 0, bpc_sweep);
     if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
         fn = blk_sweep_fn(P, ntl, 0);
         grid = update_grid(s, (const void*)fn, 0);

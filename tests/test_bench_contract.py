@@ -97,3 +97,26 @@ def test_valu_table_matches_counter_summaries():
         # the loads/stores/index arithmetic around them
         assert 6.0 < rec["instr_per_element_pivot"] < 12.0
         assert rec["f64_fma_mul_add_share"] > 0.6
+
+
+def test_two_term_arithmetic(monkeypatch):
+    """bench.two_term (the block path's VALU-vs-HBM bound) on CPU, the device query stubbed."""
+    import importlib.util
+
+    import torch
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    class Props:
+        multi_processor_count = 256
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: Props())
+    R = C = 16384
+    hbm = 16.0 * R * C
+    t = bench.two_term(R, C, 12, 8.15, 1.2e-3, hbm)
+    t_valu = R * C * 12 * 8.15 / 64 / (256 * 2.4e9)
+    t_hbm = hbm / 8e12
+    assert t["valu_peak_ms"] == pytest.approx(t_valu * 1e3)
+    assert t["hbm_peak_ms"] == pytest.approx(t_hbm * 1e3)
+    assert t["bound"] == "valu" and t["frac"] == pytest.approx(max(t_valu, t_hbm) / 1.2e-3)
+    assert bench.two_term(R, C, 4, 8.15, 1.0e-3, hbm)["bound"] == "hbm"
