@@ -20,5 +20,6 @@ cd /tmp || exit 1
   "f200|300|rocprofv3 --pmc FETCH_SIZE -d $OUT/f200 -o run --output-format csv -- $B --steps 48 --warmup 8 > /dev/null 2>&1" \
   "w200|300|rocprofv3 --pmc WRITE_SIZE -d $OUT/w200 -o run --output-format csv -- $B --steps 48 --warmup 8 > /dev/null 2>&1" \
   "f20|300|rocprofv3 --pmc FETCH_SIZE -d $OUT/f20 -o run --output-format csv -- $B --steps 20 --warmup 5 > /dev/null 2>&1" \
-  "w20|300|rocprofv3 --pmc WRITE_SIZE -d $OUT/w20 -o run --output-format csv -- $B --steps 20 --warmup 5 > /dev/null 2>&1" && \
-"$ROOT/tools/pmc_sweep.sh" "${TAG}_sq12" --pivots 12 --k 48
+  "w20|300|rocprofv3 --pmc WRITE_SIZE -d $OUT/w20 -o run --output-format csv -- $B --steps 20 --warmup 5 > /dev/null 2>&1" || exit $?
+# SKIP_SQ=1: kernel-trace and traffic passes only (the SQ passes depend on the sweep's code alone)
+[ "${SKIP_SQ:-0}" = 1 ] || "$ROOT/tools/pmc_sweep.sh" "${TAG}_sq12" --pivots 12 --k 48
