@@ -669,6 +669,13 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
                                       xhist, log_cap, st, 0, 0, xrow,
                                       light ? (int64_t)SMX_SHARD_HDR : 0);
+#ifdef SMX_BLK_TRACE_TWICE
+            // diagnostic build (tools/trace_planner.hip): a step is idempotent (it reads slot D /
+            // parity sp and writes slot L / parity sp^1), so running it again times it warm
+            if (!err && !sh)
+                err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
+                                      xhist, log_cap, st, 0, 0, xrow, 0);
+#endif
         }
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
         if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st, 0, 0, p);
