@@ -10,6 +10,9 @@
 //   3 mulpf   as 0, with the next row's multipliers loaded before this row's arithmetic
 //   4 glds    rows staged global -> LDS by global_load_lds_dwordx4 (no VGPR destination), D rows
 //             ahead per wave in an LDS ring; ds_read_b128 of the row before its arithmetic
+//   5 nostore loads and arithmetic, no stores (not compared)
+//   6 plainstore  as 0 with temporal stores;  7 tload  as 0 with temporal loads
+// (modes 3 and 4 were measured in the first run, profiles/r02/sweep_bound_probe_P*.jsonl)
 // Every compared variant is checked bit for bit against the production sweep's output.
 //
 // Build (from the repo root):
@@ -186,8 +189,17 @@ __global__ __launch_bounds__(kUpdBlock) void k_bnd(double* Tin, double* Tout, in
             x0 = *reinterpret_cast<const dbl2*>(Tin + (int64_t)i0 * ld + jl);
             v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
         }
-        if (j < C)
-            __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
+        if constexpr (MODE == 5) {
+            // loads and arithmetic, no stores: the store is kept only for a value the table never
+            // holds (so the arithmetic is not dead code)
+            if (j < C && v0[0] == 1234567.0)
+                __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
+        } else if constexpr (MODE == 6) {
+            if (j < C) *reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j) = v0;   // plain store
+        } else {
+            if (j < C)
+                __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
+        }
     };
     const int jc = min(j, (C - 1) & ~1);
     if constexpr (MODE == 3) {
@@ -229,7 +241,10 @@ __global__ __launch_bounds__(kUpdBlock) void k_bnd(double* Tin, double* Tout, in
             v = dbl2{0.25 + 1e-7 * row, -0.5 + 1e-7 * (row + lane)};
         } else {
             const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
-            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+            if constexpr (MODE == 7)   // temporal loads
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+            else
+                asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
         }
         return v;
     };
@@ -320,9 +335,9 @@ void run(int N) {
     CK(hipMalloc(&dbad, 8));
     const Var vars[] = {
         {"prod", k_bnd<P, 0, 1>, true},     {"noload", k_bnd<P, 1, 1>, false},
-        {"copy", k_bnd<P, 2, 1>, false},    {"mulpf", k_bnd<P, 3, 1>, true},
-        {"glds_d2", k_bnd<P, 4, 2>, true},  {"glds_d3", k_bnd<P, 4, 3>, true},
-        {"glds_d4", k_bnd<P, 4, 4>, true},  {"glds_d6", k_bnd<P, 4, 6>, true},
+        {"copy", k_bnd<P, 2, 1>, false},
+        {"nostore", k_bnd<P, 5, 1>, false}, {"plainstore", k_bnd<P, 6, 1>, true},
+        {"tload", k_bnd<P, 7, 1>, true},
     };
     const int nchunks = (C + 2 * kWave - 1) / (2 * kWave);
     for (const Var& v : vars) {
