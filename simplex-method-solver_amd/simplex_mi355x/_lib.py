@@ -66,6 +66,7 @@ EXPORTS = (
     "smx_tune_resident", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check",
     "smx_tune_block", "smx_tune_block_pipe", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
+    "smx_block_timed_read",
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
@@ -148,6 +149,8 @@ def load():
         "smx_block_run_timed": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp,
                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)],
                                 ctypes.c_int),
+        "smx_block_timed_read": ([i32, ctypes.POINTER(ctypes.c_float),
+                                  ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "smx_block_graph_create": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp,
                                     ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "smx_bshard_bytes": ([sp], ctypes.c_int64),

@@ -271,30 +271,48 @@ class DeviceTableau:
         self._graphs[(parity, k, "blk", pivots)] = g
         return g
 
-    def run_block_timed(self, k: int, pivots: int):
-        """k chained pivots in blocks of ``pivots`` with HIP events around every sweep
-        (synchronous).  Returns (per-sweep ms array, device ms of the whole chain)."""
+    def block_timed_launcher(self, k: int, pivots: int):
+        """``run_block_timed`` in two calls: the host preparation (shape, plan, scratch) is done
+        here; returns (launch, read).  ``launch()`` only enqueues the chain with its HIP events
+        (smx_block_run_timed with NULL outputs); ``read()`` waits for the chain's last event and
+        returns (per-sweep ms array, device ms of the whole chain).  A timed region can bracket
+        launch() and its own synchronize, with the event readout after it."""
         import ctypes
         self.settle()
         if self._term:
             self.clear_term()
         p = self.step & 1
         nb = -(-k // pivots)
-        sw = (ctypes.c_float * nb)()
-        tot = ctypes.c_float()
         plan = _lib.block_plan(self.shape, pivots)
         if plan is None:
             raise ValueError(f"shape {self.shape} is not eligible for block pivots")
         blk = self._blk_for(plan)
         sh = ops.make_shape(self.shape)
-        _lib.check(_lib.load().smx_block_run_timed(
-            self.buf[0].data_ptr(), self.buf[1].data_ptr(), ctypes.byref(sh), p, k, pivots,
-            self.ctl.data_ptr(), blk.data_ptr(), blk.numel() * 8, self.log.data_ptr(),
-            self.xhist.data_ptr(), self.log_cap, self.stream.cuda_stream, sw,
-            ctypes.byref(tot)), "smx_block_run_timed")
-        self.step += k
-        self._pending = True
-        return np.frombuffer(sw, dtype=np.float32).copy(), float(tot.value)
+        L = _lib.load()
+        args = (self.buf[0].data_ptr(), self.buf[1].data_ptr(), ctypes.byref(sh), p, k, pivots,
+                self.ctl.data_ptr(), blk.data_ptr(), blk.numel() * 8, self.log.data_ptr(),
+                self.xhist.data_ptr(), self.log_cap, self.stream.cuda_stream)
+
+        def launch() -> None:
+            _lib.check(L.smx_block_run_timed(*args, None, None), "smx_block_run_timed")
+            self.step += k
+            self._pending = True
+
+        def read():
+            sw = (ctypes.c_float * nb)()
+            tot = ctypes.c_float()
+            _lib.check(L.smx_block_timed_read(nb, sw, ctypes.byref(tot)), "smx_block_timed_read")
+            return np.frombuffer(sw, dtype=np.float32).copy(), float(tot.value)
+
+        launch.shape = sh   # keeps the ctypes shape alive as long as the closures
+        return launch, read
+
+    def run_block_timed(self, k: int, pivots: int):
+        """k chained pivots in blocks of ``pivots`` with HIP events around every sweep
+        (synchronous).  Returns (per-sweep ms array, device ms of the whole chain)."""
+        launch, read = self.block_timed_launcher(k, pivots)
+        launch()
+        return read()
 
     def _xch_for(self, plan) -> torch.Tensor:
         nbytes = plan[0]

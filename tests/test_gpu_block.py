@@ -226,3 +226,36 @@ def test_block_plan_policy(block_mode):
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 17) is None
     block_mode(1)
     assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64]) is None
+
+
+def test_deferred_timed_launch_vs_oracle(block_mode):
+    """The bench's timed form: block_timed_launcher's launch() only enqueues (smx_block_run_timed
+    with NULL outputs), read() waits and returns the sweep times; the table bit-exact against
+    the C oracle, and a read without a deferred launch is refused."""
+    import ctypes
+
+    import torch
+    from oracle import c_oracle
+    from simplex_mi355x import _lib, lp
+    from simplex_mi355x.device import DeviceTableau
+    block_mode(0)
+    n = m = 3071
+    k = 13
+    T = lp.dense_tableau("uniform", 0, n, m)
+    dev = DeviceTableau(T, n, m, m)
+    P = dev.block_plan()[1]
+    launch, read = dev.block_timed_launcher(k, P)
+    launch()
+    torch.cuda.synchronize()
+    sw, tot = read()
+    assert len(sw) == -(-k // P) and (sw > 0).all() and tot >= float(sw.sum())
+    f = ctypes.c_float()
+    assert _lib.load().smx_block_timed_read(len(sw), (ctypes.c_float * len(sw))(),
+                                            ctypes.byref(f)) != 0      # already read
+    ctl = dev.sync_state()
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=16)
+    assert int(ctl["npivots"]) == done == k
+    assert np.array_equal(dev.read_log(0, k), log)
+    got = dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
