@@ -56,10 +56,16 @@ namespace {
 
 // ---------------------------------------------------------------------------------------------
 inline int nparts_for(int rows, int m) {
+    // SMX_NPARTS_MAX (experiments): a lower cap on the select / planner workgroup count
+    static const int cap_env = [] {
+        const char* e = getenv("SMX_NPARTS_MAX");
+        return e ? atoi(e) : 0;
+    }();
     const int work = rows > m ? rows : m;
     int p = (work + kSelBlock - 1) / kSelBlock;
     if (p < 1) p = 1;
     if (p > kMaxParts) p = kMaxParts;
+    if (cap_env > 0 && p > cap_env) p = cap_env;
     return p;
 }
 
