@@ -299,6 +299,12 @@ int smx_resident_run(double* buf0, double* buf1, const smx_shape* shape, int32_t
  * out[1] = pairs whose results differ in any bit (device unsigned long long[2]). */
 int smx_fastdiv_check(const double* num, const double* den, int64_t count,
                       unsigned long long* out, void* stream);
+/* The block sweep's unchecked division (smx_block.hpp, kBndSpan: no per-element window when the
+ * pivot elements, pivot-row values and multipliers are bounded) against num / den on the domain
+ * those bounds guarantee: den in [2^-100, 2^101), num = +0 or |num| in [2^-254, 2^410).
+ * out[0] = pairs inside the domain, out[1] = those that differ in any bit.  Test support. */
+int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t count,
+                              unsigned long long* out, void* stream);
 
 /* ---- block pivots: P pivots per HBM sweep ------------------------------------------------
  * k pivots of the get_solution loop (simplex.py:184-198) in blocks of `pivots` (1..16): per block,

@@ -126,6 +126,60 @@ __device__ __forceinline__ uint32_t win_term(double n) {
     return t;
 }
 
+// Bounded operands: the sweep's unchecked fast path (blk_sweep_body_row1).  A unit needs no
+// per-element window tracking when every pivot element e_q, every pivot-row value p_q[j] of the
+// wave's chunk and every multiplier mq_q of the row lies in [2^-100, 2^101) in magnitude (bnd_term
+// < kBndSpan; zeros, denormals, infinities and NaN fall outside) and the unit's input elements are
+// finite with |x| < 2^101 (zeros and denormals allowed).  Then every numerator of the chain
+//     num = RN(RN(x_q * e) - RN(p * mq)),   x_{q+1} = num / e
+// is +0 or inside [2^-254, 2^410):
+//   * b = RN(p * mq) is normal with |b| in [2^-200, 2^202];
+//   * |a| <= |b| / 2 or |a| >= 2 |b|: |num| >= |b| / 2 (no cancellation); otherwise a - b is exact
+//     (Sterbenz) and, unless 0, at least one ulp of |b| / 2 >= 2^-254.  num = -0 needs b = +0, so
+//     a zero numerator is +0;
+//   * |x_{q+1}| <= (|x_q| + |b / e|)(1 + 2^-52) <= 2^101 + 16 * 2^303 < 2^308 over 16 steps, so
+//     |a| < 2^409 and |num| < 2^410.
+// There the hoisted-reciprocal division (t = num y, r = fma(-e, t, num), fma(r, y, t)) is the
+// compiler's own sequence with no scaling step (numerator exponent far above 53, exponent
+// difference below 768, quotient normal) and no fixup case (a +0 numerator gives t's sign, which
+// is sign(num) xor sign(e)): bit-identical to num / e (tests/test_gpu_resident.py checks the
+// sequence on this domain).  Units outside these bounds keep the window-tracked path.
+// SMX_BLK_NOFREE=1 in the environment (read at the first block launch): every unit takes the
+// window-tracked path, for A/B timing on one box (tools/block_bench.py)
+__device__ int g_blk_nofree = 0;
+constexpr uint32_t kBndBias = 0u - (923u << 21);   // 2^-100 (biased exponent 923) -> 0
+constexpr uint32_t kBndSpan = 201u << 21;          // up to biased exponent 1123 (2^101 excluded)
+constexpr uint32_t kBndXMax = 1124u << 21;         // (hi << 1) below this: |x| < 2^101, finite
+__device__ __forceinline__ uint32_t bnd_term(double v) {
+    return ((uint32_t)__double2hiint(v) << 1) + kBndBias;
+}
+
+// Self-check of the unchecked sequence on the domain the bounds guarantee (smx_fastdiv_check
+// bounded): out[0] = pairs with e in [2^-100, 2^101) and num = +0 or |num| in [2^-254, 2^410),
+// out[1] = those whose unchecked quotient differs from num / e in any bit.
+__global__ __launch_bounds__(256) void k_fastdiv_bounded_check(const double* __restrict__ num,
+                                                               const double* __restrict__ den,
+                                                               int64_t count,
+                                                               unsigned long long* __restrict__ out) {
+    unsigned long long in = 0, bad = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double x = num[i], e = den[i];
+        const uint32_t xe = ((uint32_t)(dbits(x) >> 52)) & 0x7ffu;
+        const bool dom = bnd_term(e) < kBndSpan &&
+                         (dbits(x) == 0 || (xe >= 1023u - 254u && xe < 1023u + 410u));
+        if (!dom) continue;
+        const FastDiv f = fd_prep(e);
+        const double t = x * f.y;
+        const double r = fma(-e, t, x);
+        const double q = fma(r, f.y, t);
+        ++in;
+        bad += (dbits(q) != dbits(x / e)) ? 1 : 0;
+    }
+    atomicAdd(&out[0], in);
+    atomicAdd(&out[1], bad);
+}
+
 
 // chain() with the division in its hoisted-reciprocal form (3 dependent fp64 ops instead of the
 // ~10 of the IEEE sequence): bit-identical while every numerator stays inside the window, which
@@ -1301,6 +1355,17 @@ __device__ __forceinline__ void blk_sweep_body_row1(const double* Tin, double* T
         cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
     }
     const bool cspecial = !allok;
+    // the unchecked fast path (kBndSpan) for this wave's chunk: bounded pivot elements and
+    // pivot-row values, no pivot column in the chunk (g_blk_nofree: A/B experiments only)
+    const bool kNoFree = g_blk_nofree != 0;
+    uint32_t pt = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        pt = max(pt, bnd_term(eq[q]));
+        if (j < C) pt = max(pt, bnd_term(prs[q][0]));
+        if (j + 1 < C) pt = max(pt, bnd_term(prs[q][1]));
+    }
+    const bool chunk_free = !kNoFree && !colchunk && __all(pt < kBndSpan);
     const int base = w / nchunks;
     const int tbq = blk_special_batch<P, 1>(h, base, qs);
     int tsp = blk_next_batch<P>(tbq, -1);
@@ -1309,10 +1374,32 @@ __device__ __forceinline__ void blk_sweep_body_row1(const double* Tin, double* T
         double pc0[P];
         const bool special = cspecial || t == tsp;
         if (t == tsp) tsp = blk_next_batch<P>(tbq, t);
+        uint32_t mt = 0;   // the row's multipliers (uniform: scalar ops)
 #pragma unroll
-        for (int q = 0; q < P; ++q) pc0[q] = m0[q];
+        for (int q = 0; q < P; ++q) {
+            pc0[q] = m0[q];
+            mt = max(mt, bnd_term(pc0[q]));
+        }
         dbl2 v0 = x0;
         bool ok = false;
+        auto fast_free = [&]() {
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const double e = eq[q], y = yq[q];
+                double n[2];
+                n[0] = v0[0] * e - prs[q][0] * pc0[q];
+                n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                double rr[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const double tq = n[k] * y;
+                    const double r = fma(-e, tq, n[k]);
+                    rr[k] = fma(r, y, tq);
+                }
+                v0 = dbl2{rr[0], rr[1]};
+            }
+            ok = true;
+        };
         auto fast = [&](auto selc) {
             constexpr bool SEL = decltype(selc)::value;
             uint32_t wt = 0;
@@ -1340,7 +1427,11 @@ __device__ __forceinline__ void blk_sweep_body_row1(const double* Tin, double* T
             ok = __all(wt < kWinSpan);
         };
         if (!special) {
-            if (colchunk)
+            const uint32_t xt = max((uint32_t)__double2hiint(x0[0]) << 1,
+                                    (uint32_t)__double2hiint(x0[1]) << 1);
+            if (chunk_free && mt < kBndSpan && __all(xt < kBndXMax))
+                fast_free();
+            else if (colchunk)
                 fast(SmxBool<true>{});
             else
                 fast(SmxBool<false>{});

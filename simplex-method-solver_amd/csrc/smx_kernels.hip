@@ -1464,6 +1464,16 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
     return (int)hipGetLastError();
 }
 
+int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t count,
+                              unsigned long long* out, void* stream) {
+    if (count < 0 || !num || !den || !out) return (int)hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), S(stream));
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_fastdiv_bounded_check, dim3(1024), dim3(256), 0, S(stream), num, den,
+                       count, out);
+    return (int)hipGetLastError();
+}
+
 int smx_tune_block_pipe(int32_t on) {
     const int prev = g_block_pipe;
     if (on >= 0) g_block_pipe = on ? 1 : 0;
@@ -1477,6 +1487,14 @@ int smx_tune_block(int32_t pivots) {
 }
 
 int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout) {
+    // SMX_BLK_NOFREE=1 (A/B experiments): set once, here, outside any stream capture
+    static const int nofree_env = [] {
+        const char* e = getenv("SMX_BLK_NOFREE");
+        const int v = (e && e[0] == '1') ? 1 : 0;
+        if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_blk_nofree), &v, sizeof v);
+        return v;
+    }();
+    (void)nofree_env;
     if (!shape_ok(shape)) return 0;
     const int req = pivots_inout ? *pivots_inout : 0;
     if (req < 0 || req > kBlkMax) return 0;

@@ -64,7 +64,7 @@ EXPORTS = (
     "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
     "smx_tune_resident", "smx_resident_trace", "smx_resident_bytes",
-    "smx_resident_run", "smx_fastdiv_check",
+    "smx_resident_run", "smx_fastdiv_check", "smx_fastdiv_check_bounded",
     "smx_tune_block", "smx_tune_block_pipe", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
     "smx_block_graph_create",
@@ -141,6 +141,7 @@ def load():
         "smx_resident_run": ([vp, vp, sp, i32, i32, vp, vp, i64, i32, vp, vp, i64, vp],
                              ctypes.c_int),
         "smx_fastdiv_check": ([vp, vp, i64, vp, vp], ctypes.c_int),
+        "smx_fastdiv_check_bounded": ([vp, vp, i64, vp, vp], ctypes.c_int),
         "smx_tune_block": ([i32], ctypes.c_int),
         "smx_tune_block_pipe": ([i32], ctypes.c_int),
         "smx_block_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),

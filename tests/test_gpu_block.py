@@ -99,6 +99,36 @@ def test_block_vs_oracle(block_mode, kind, n, m, k, chunk, P):
     assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
 
 
+@pytest.mark.parametrize("P", [10, 12, 16])
+def test_block_bounded_fast_path_edges_vs_oracle(block_mode, P):
+    """The one-row sweep's unchecked fast path (smx_block.hpp, kBndSpan) next to its fallbacks in
+    one table: rows scaled past 2^101 (input bound), rows scaled to ~2^-60 (small numerators),
+    columns scaled to ~2^-99 (pivot-row values below 2^-100: the chunk falls back), exact zeros
+    (zero multipliers and pivot-row values), signed zeros -- bit-exact against the C oracle."""
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    import simplex
+    block_mode(P)
+    n = m = 1023
+    T = lp.dense_tableau("uniform", 5, n, m)
+    T[0:40] *= 2.0 ** 102
+    T[40:90] *= 2.0 ** -60
+    T[:, 200:260] *= 2.0 ** -99
+    T[300:340, 500:540] = 0.0
+    T[340:350, 600:640] = -0.0
+    T[500:900, 700] = 0.0
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    assert sm._dev.block_plan()[1] == P
+    k = 4 * P + 3
+    sm.solve(record_history=False, max_pivots=k, chunk=k)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    assert sm.pivots == done
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    got = sm._dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
 @pytest.mark.parametrize("P", [1, 2, 5, 8, 16])
 def test_graph_and_eager_block_chains_agree(block_mode, P):
     from simplex_mi355x import lp

@@ -202,6 +202,41 @@ def test_fastdiv_matches_hardware_division():
     assert inside > num.size // 2
 
 
+def test_fastdiv_bounded_domain_matches_hardware_division():
+    """The block sweep's unchecked fast path (smx_block.hpp, kBndSpan) divides with no window
+    check when the pivot elements, pivot-row values and multipliers are bounded, which keeps
+    every numerator at +0 or inside [2^-254, 2^410) and the pivot element inside [2^-100, 2^101):
+    the hoisted-reciprocal sequence must equal x / e bit for bit on that whole domain -- random
+    mantissas and signs across it, its edges, all-ones and power-of-two mantissas, +0."""
+    import torch
+    from simplex_mi355x import _lib
+    rng = np.random.default_rng(321)
+    N = 1 << 22
+
+    def mk(exp_lo, exp_hi, mant=None):
+        m = rng.random(N) + 1.0 if mant is None else mant
+        x = np.ldexp(m, rng.integers(exp_lo, exp_hi, N))
+        return np.where(rng.random(N) < 0.5, -x, x)
+
+    ones = np.full(N, 2.0 - 2.0 ** -52)
+    nums = [mk(-254, 410), mk(-254, -240), mk(395, 410), mk(-254, 410, ones),
+            mk(-254, 410, np.full(N, 1.0)), mk(-3, 4)]
+    dens = [mk(-100, 101), mk(90, 101), mk(-100, -90), mk(-100, 101, ones),
+            mk(-100, 101, np.full(N, 1.0 + 2.0 ** -52)), rng.uniform(-1, 1, N)]
+    num = np.concatenate(nums)
+    den = np.concatenate(dens)
+    num[::97] = 0.0                    # +0 numerators (a zero numerator is never -0 there)
+    tn = torch.from_numpy(num).cuda()
+    td = torch.from_numpy(den).cuda()
+    out = torch.zeros(2, dtype=torch.int64, device="cuda")
+    _lib.check(_lib.load().smx_fastdiv_check_bounded(
+        tn.data_ptr(), td.data_ptr(), num.size, out.data_ptr(),
+        torch.cuda.current_stream().cuda_stream), "smx_fastdiv_check_bounded")
+    inside, bad = (int(x) for x in out.cpu())
+    assert bad == 0
+    assert inside > 0.95 * num.size
+
+
 def test_two_resident_chains_on_separate_streams(resident_mode):
     """Two solvers, each on its own stream, enqueue resident chains that overlap in time: every
     workgroup of a chain must be resident at once (256 of them each at 1023^2), so the library
