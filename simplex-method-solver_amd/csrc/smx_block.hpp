@@ -1159,6 +1159,15 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
         cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
     }
     const bool cspecial = !allok;
+    // the unchecked fast path for this wave's chunk (kBndSpan; as blk_sweep_body_row1)
+    uint32_t pt = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        pt = max(pt, bnd_term(eq[q]));
+        if (j < C) pt = max(pt, bnd_term(prs[q][0]));
+        if (j + 1 < C) pt = max(pt, bnd_term(prs[q][1]));
+    }
+    const bool chunk_free = g_blk_nofree == 0 && !colchunk && __all(pt < kBndSpan);
     const int base = w / nchunks;
     const int tbq = blk_special_batch<P>(h, base, qs);
     int tsp = blk_next_batch<P>(tbq, -1);
@@ -1171,13 +1180,36 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
         double pc0[P], pc1[P];
         const bool special = cspecial || !h1 || t == tsp;
         if (t == tsp) tsp = blk_next_batch<P>(tbq, t);
+        uint32_t mt = 0;   // the two rows' multipliers (uniform: scalar ops)
 #pragma unroll
         for (int q = 0; q < P; ++q) {
             pc0[q] = m0[q];
             pc1[q] = m1[q];
+            mt = max(mt, max(bnd_term(pc0[q]), bnd_term(pc1[q])));
         }
         dbl2 v0 = x0, v1 = x1;
         bool ok = false;
+        auto fast_free = [&]() {
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const double e = eq[q], y = yq[q];
+                double n[4];
+                n[0] = v0[0] * e - prs[q][0] * pc0[q];
+                n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                n[2] = v1[0] * e - prs[q][0] * pc1[q];
+                n[3] = v1[1] * e - prs[q][1] * pc1[q];
+                double rr[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double tq = n[k] * y;
+                    const double r = fma(-e, tq, n[k]);
+                    rr[k] = fma(r, y, tq);
+                }
+                v0 = dbl2{rr[0], rr[1]};
+                v1 = dbl2{rr[2], rr[3]};
+            }
+            ok = true;
+        };
         // the fast path: numerators in the window form, one integer window term per element
         auto fast = [&](auto selc) {
             constexpr bool SEL = decltype(selc)::value;
@@ -1211,7 +1243,13 @@ __device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* 
             ok = __all(wt < kWinSpan);   // NaN / inf / zero numerators fall outside the window
         };
         if (!special) {
-            if (colchunk)
+            const uint32_t xt = max(max((uint32_t)__double2hiint(x0[0]) << 1,
+                                        (uint32_t)__double2hiint(x0[1]) << 1),
+                                    max((uint32_t)__double2hiint(x1[0]) << 1,
+                                        (uint32_t)__double2hiint(x1[1]) << 1));
+            if (chunk_free && mt < kBndSpan && __all(xt < kBndXMax))
+                fast_free();
+            else if (colchunk)
                 fast(SmxBool<true>{});
             else
                 fast(SmxBool<false>{});
