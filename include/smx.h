@@ -269,6 +269,13 @@ int smx_shard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
                         int32_t nranks, void* comm, int32_t* log, int64_t log_cap, void* stream,
                         float* host_update_ms, float* host_total_ms);
 
+/* The resident loop's hand-off spin bound in s_memrealtime ticks (100 MHz; default 2 s) on the
+ * current device: ticks >= 0 sets it, < 0 only queries.  Returns the previous bound (-1 on a HIP
+ * error).  A spin past the bound latches ctl.dec[0][0] and the grid drains; the Python host then
+ * restores the chain's input from its snapshot and reruns the pivots on the launch chain
+ * (device.py).  Test support: a bound of 0 forces that path. */
+int64_t smx_tune_resident_timeout(int64_t ticks);
+
 /* ---- on-chip resident pivot loop ---------------------------------------------------------
  * The whole get_solution pivot loop (simplex.py:184-198) for k pivots in ONE persistent launch:
  * G workgroups (one per CU, 1024 threads) each hold ceil(n/G) constraint rows and a replica of

@@ -1428,6 +1428,16 @@ int smx_tune_resident(int32_t workgroups) {
     return prev;
 }
 
+int64_t smx_tune_resident_timeout(int64_t ticks) {
+    int64_t prev = -1;
+    if (hipMemcpyFromSymbol(&prev, HIP_SYMBOL(g_res_spin_ticks), sizeof prev) != hipSuccess)
+        return -1;
+    if (ticks >= 0 &&
+        hipMemcpyToSymbol(HIP_SYMBOL(g_res_spin_ticks), &ticks, sizeof ticks) != hipSuccess)
+        return -1;
+    return prev;
+}
+
 int smx_resident_trace(void* trace, int32_t from_step) {
     g_resident_trace = static_cast<uint64_t*>(trace);
     g_resident_trace_from = from_step < 0 ? 0 : from_step;

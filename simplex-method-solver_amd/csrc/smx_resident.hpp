@@ -41,6 +41,9 @@ constexpr int kResWaves = kResBlock / kWave;
 constexpr int kResPollers = 256;                 // records polled by threads 0..G-1 (G <= 256)
 constexpr int kResRecWords = 4;                  // 32-B record: 4 granules
 constexpr int64_t kResSpinTicks = 200000000;     // 2 s of s_memrealtime (100 MHz)
+// The bound every spin uses (smx_tune_resident_timeout; tests shorten it to force the timeout
+// and exercise the host's recovery, device.py)
+__device__ int64_t g_res_spin_ticks = kResSpinTicks;
 constexpr int kResTimeout = 1;                   // ctl->dec[0][0]: a hand-off timed out
 constexpr int kResMaxRows = 65534;               // 16-bit row fields in the record
 constexpr int kResTraceSteps = 64;               // diagnostic trace: steps recorded
@@ -349,7 +352,7 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
 #pragma unroll
                 for (int q = 0; q < kResRecWords; ++q) ok = ok && (uint32_t)(w[q] >> 32) == want;
                 if (ok) break;
-                if (rt_now() - t0 > kResSpinTicks) {
+                if (rt_now() - t0 > g_res_spin_ticks) {
                     s_err = 1;
                     break;
                 }

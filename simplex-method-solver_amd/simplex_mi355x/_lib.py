@@ -63,7 +63,7 @@ EXPORTS = (
     "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
     "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
-    "smx_tune_resident", "smx_resident_trace", "smx_resident_bytes",
+    "smx_tune_resident", "smx_tune_resident_timeout", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check", "smx_fastdiv_check_bounded",
     "smx_tune_block", "smx_tune_block_pipe", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
@@ -136,6 +136,7 @@ def load():
         "smx_shard_folds_pack": ([sp], ctypes.c_int),
         "smx_tune_fold": ([i64], ctypes.c_int64),
         "smx_tune_resident": ([i32], ctypes.c_int),
+        "smx_tune_resident_timeout": ([i64], ctypes.c_int64),
         "smx_resident_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
         "smx_resident_trace": ([vp, i32], ctypes.c_int),
         "smx_resident_run": ([vp, vp, sp, i32, i32, vp, vp, i64, i32, vp, vp, i64, vp],

@@ -94,6 +94,10 @@ class DeviceTableau:
         self.resident = resident
         self._xch = None
         self._epoch = 0
+        # the input of a resident chain not yet confirmed (buffer, control block, step, pivots):
+        # on a hand-off timeout sync_state restores it and reruns the pivots on the launch chain
+        self._res_snap = None
+        self.resident_fallbacks = 0
         # None: the library's policy (smx_tune_block); 0: never; 1..16: pivots per sweep
         self.block = block
         self._blk = None
@@ -212,6 +216,9 @@ class DeviceTableau:
         with torch.cuda.stream(self.stream):
             if plan is not None:
                 xch, epoch = self._xch_for(plan), self._next_epoch()
+                # a copy of the chain's input (tables up to ~1920^2: <= 30 MB, ~0.1 % of the
+                # chain's time) so a hand-off timeout is recoverable (sync_state)
+                self._res_snap = (self.buf[p].clone(), self.ctl.clone(), self.step, k)
                 ops.resident_run(self.buf, self.ctl, xch, self.log, self.xhist, self.shape, p,
                                  k, epoch)
             elif bplan is not None:
@@ -374,10 +381,26 @@ class DeviceTableau:
     def sync_state(self) -> np.void:
         """Read the control block and set the host step counter to the device pivot count."""
         c = self.read_ctl()
+        snap, self._res_snap = self._res_snap, None
         if int(c["dec"][0][0]) & _lib.RESIDENT_TIMEOUT:
             self._pending = False
-            raise RuntimeError("resident pivot loop: a workgroup hand-off timed out (the "
-                               "tableau on the device is undefined)")
+            if snap is None:
+                raise RuntimeError("resident pivot loop: a workgroup hand-off timed out (the "
+                                   "tableau on the device is undefined)")
+            # the chain's workgroups could not all be resident at once (or one stalled): put
+            # its input back and run the same pivots on the launch chain, for good on this
+            # tableau -- the same decisions and arithmetic, so the same results
+            buf_in, ctl_in, step0, k = snap
+            with torch.cuda.stream(self.stream):
+                self.buf[step0 & 1].copy_(buf_in)
+                self.ctl.copy_(ctl_in)
+            del buf_in, ctl_in
+            self.step = step0
+            self._term = False
+            self.resident = False
+            self.resident_fallbacks += 1
+            self.run(k)
+            return self.sync_state()
         self.step = int(c["npivots"])
         self._pending = False
         self._term = bool(c["term"])

@@ -61,6 +61,36 @@ def test_every_fixture_resident_vs_chain_vs_reference(resident_mode):
     assert n_res > 250
 
 
+def test_hand_off_timeout_recovers_on_launch_chain(resident_mode):
+    """A resident chain whose hand-off spin times out (forced here: smx_tune_resident_timeout(0))
+    leaves its table undefined; the host restores the chain's input from the snapshot it took,
+    reruns the same pivots on the launch chain and keeps that tableau off the resident loop --
+    results bit-exact against the C oracle, across several chunks."""
+    from oracle import c_oracle
+    from simplex_mi355x import _lib, lp
+    import simplex
+    n, m, k = 511, 511, 90
+    T = lp.dense_tableau("mixed", 9, n, m)
+    resident_mode(0)
+    L = _lib.load()
+    prev = int(L.smx_tune_resident_timeout(0))
+    assert prev > 0
+    try:
+        sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+        assert sm._dev.resident_plan() is not None
+        sm.solve(record_history=False, max_pivots=k, chunk=30)
+    finally:
+        assert int(L.smx_tune_resident_timeout(prev)) == 0
+    assert sm._dev.resident_fallbacks == 1
+    assert sm._dev.resident is False
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    assert sm.pivots == done
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    got = sm._dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
 @pytest.mark.parametrize("wg", [1, 3, 7, 64, 255, 256])
 def test_workgroup_counts_agree(resident_mode, wg):
     """Any grid (1 .. 256 workgroups, ragged last row block) gives the same bits."""
