@@ -144,7 +144,8 @@ __device__ __forceinline__ uint32_t win_term(double n) {
 // difference below 768, quotient normal) and no fixup case (a +0 numerator gives t's sign, which
 // is sign(num) xor sign(e)): bit-identical to num / e (tests/test_gpu_resident.py checks the
 // sequence on this domain).  Units outside these bounds keep the window-tracked path.
-// SMX_BLK_NOFREE=1 in the environment (read at the first block launch): every unit takes the
+// SMX_BLK_NOFREE=1 in the environment (read once, by the first smx_block_bytes call -- outside any
+// stream capture, since the device-symbol write would invalidate one): every unit takes the
 // window-tracked path, for A/B timing on one box (tools/block_bench.py)
 __device__ int g_blk_nofree = 0;
 constexpr uint32_t kBndBias = 0u - (923u << 21);   // 2^-100 (biased exponent 923) -> 0

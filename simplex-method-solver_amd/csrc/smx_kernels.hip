@@ -823,10 +823,26 @@ struct Graph {
 
 // Timing events of the *_run_timed calls: created once (smx_timer_reserve, or on first need) and
 // reused, so no hipEventCreate / hipEventDestroy runs inside a caller's timed region.
+// The pool belongs to the device that was current when it was filled; a caller on another device
+// gets a fresh pool there.  Any new use of the pool invalidates a pending deferred block readout
+// (smx_block_run_timed with NULL outputs -> smx_block_timed_read), which would otherwise read
+// events that the new caller re-recorded.
 hipEvent_t* g_timer_ev = nullptr;
 size_t g_timer_n = 0;
+int g_timer_dev = -1;
+int g_timed_blocks = 0;   // blocks of the pending deferred smx_block_run_timed (0: none)
 
 int timer_events(size_t n, hipEvent_t** out) {
+    g_timed_blocks = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1;
+    if (g_timer_n && dev != g_timer_dev) {
+        (void)hipSetDevice(g_timer_dev);
+        for (size_t i = 0; i < g_timer_n; ++i) (void)hipEventDestroy(g_timer_ev[i]);
+        (void)hipSetDevice(dev);
+        g_timer_n = 0;
+    }
+    g_timer_dev = dev;
     if (n > g_timer_n) {
         hipEvent_t* grown = static_cast<hipEvent_t*>(realloc(g_timer_ev, n * sizeof(hipEvent_t)));
         if (!grown) return 1;
@@ -1524,9 +1540,6 @@ int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
                             static_cast<char*>(blk), log, xhist, log_cap, S(stream));
 }
 
-// blocks of the last deferred smx_block_run_timed (0: none to read)
-static int g_timed_blocks = 0;
-
 static int block_timed_read(int nb, float* host_sweep_ms, float* host_total_ms) {
     hipEvent_t* ev = g_timer_ev;
     int err = (int)hipEventSynchronize(ev[2 * nb + 1]);
@@ -1550,7 +1563,6 @@ int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     hipStream_t st = S(stream);
     const int nb = (k + pivots - 1) / pivots;
     hipEvent_t* ev = nullptr;
-    g_timed_blocks = 0;
     if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * nb], st);
     int err = launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,

@@ -231,8 +231,8 @@ def tune_block(pivots: int = -1) -> int:
 
 
 def tune_block_pipe(on: int = -1) -> int:
-    """smx_tune_block_pipe: 1 plan the next block on a second stream during each sweep (the
-    default), 0 plan every block on the solver stream, -1 query only; returns the previous
+    """smx_tune_block_pipe: 0 plan every block on the solver stream (the default), 1 plan the
+    next block on a second stream during each sweep (opt-in), -1 query only; returns the previous
     setting."""
     return int(load().smx_tune_block_pipe(on))
 

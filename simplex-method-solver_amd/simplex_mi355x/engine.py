@@ -176,18 +176,32 @@ def _dense_from_lists(constraints, function, m):
 
 def _use_host(device) -> bool:
     """The host engine runs a tableau only on request (``device="cpu"``) or when this machine has
-    no HIP device at all; with an MI355X present every tableau lives in HBM."""
+    no HIP device at all -- then with a one-time ``RuntimeWarning``, and ``SimplexMethod.backend``
+    reads "host"; with an MI355X present every tableau lives in HBM."""
     if device is not None:
         return str(device) == "cpu"
     import torch
-    return not torch.cuda.is_available()
+    if torch.cuda.is_available():
+        return False
+    global _warned_host
+    if not _warned_host:
+        _warned_host = True
+        import warnings
+        warnings.warn("simplex_mi355x: no HIP device is visible, so SimplexMethod runs on the host "
+                      "engine (backend == 'host'); pass device='cpu' to choose it explicitly",
+                      RuntimeWarning, stacklevel=3)
+    return True
+
+
+_warned_host = False
 
 
 class SimplexMethod:
     """simplex.py:24-199 on an MI355X-resident tableau (or, on a machine without one, on the
     host engine of the same library: ``backend == "host"``)."""
 
-    def __init__(self, constraints, function, device=None, devices=None, pivots=None):
+    def __init__(self, constraints, function, device=None, devices=None, pivots=None,
+                 exchange=None):
         # simplex.py:26-33 (IndexError on an empty constraint list, like the reference)
         self.n = len(constraints)
         self.m = len(constraints[0]) - 1
@@ -208,7 +222,8 @@ class SimplexMethod:
         if devices is not None:
             # row sharding behind the same surface: rank p's rows on devices[p] (multi.py)
             from .multi import MultiTableau
-            self._dev = MultiTableau(dense, self.n, self.m, self.flen, devices, pivots=pivots)
+            self._dev = MultiTableau(dense, self.n, self.m, self.flen, devices, pivots=pivots,
+                                     exchange=exchange)
         elif _use_host(device):
             from .host import HostTableau
             self._dev = HostTableau(dense, self.n, self.m, self.flen)

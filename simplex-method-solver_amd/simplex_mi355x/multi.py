@@ -100,6 +100,7 @@ class MultiTableau:
         self._saved = None        # control blocks before a pick() not yet applied
         self._xcodes = self._initial_codes()
         self._xstep = 0           # pivot count _xcodes describes
+        self._xck = {0: self._xcodes}   # label codes at earlier read_xhist stops (see there)
 
     # -- native rank table --------------------------------------------------------------------
     def _rank_structs(self):
@@ -139,6 +140,7 @@ class MultiTableau:
         self._saved = None
         self._xcodes = self._initial_codes()
         self._xstep = 0
+        self._xck = {0: self._xcodes}
 
     def settle(self) -> None:
         for be in self.ranks:
@@ -190,9 +192,16 @@ class MultiTableau:
         if stop <= start:
             return np.zeros((0, 2), dtype=np.float64)
         if start != self._xstep:
-            # re-derive the label positions at `start` from the log (only the ring's window)
-            codes = self._initial_codes()
-            for r, c in self.read_log(0, start):
+            # re-derive the label positions at `start`: from the nearest earlier stop whose
+            # codes were kept, replaying the pivots after it -- which must still be in the
+            # device's log ring (log_cap entries; older ones are overwritten)
+            s0 = max(k for k in self._xck if k <= start)
+            if max(self.step, stop) - s0 > self.log_cap:
+                raise RuntimeError(
+                    f"x-history from pivot {start}: the pivots after {s0} are no longer in the "
+                    f"device log ring (log_cap = {self.log_cap}); read the history in order")
+            codes = list(self._xck[s0])
+            for r, c in self.read_log(s0, start):
                 codes = [None if x is None else _move(x, int(r), int(c)) for x in codes]
             self._xcodes, self._xstep = codes, start
         log = self.read_log(start, stop)
@@ -206,6 +215,10 @@ class MultiTableau:
                     p, _ = self._owner(x)
                     out[t, q] = rings[p][t, q]
         self._xcodes, self._xstep = codes, stop
+        self._xck[stop] = codes
+        if len(self._xck) > 64:   # keep the start and the newest stops
+            for k in sorted(self._xck)[1:-32]:
+                del self._xck[k]
         return out
 
     def block_plan(self):

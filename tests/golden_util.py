@@ -104,3 +104,29 @@ def trajectory_cap(rec) -> int:
     """Pivots to run so a replay ends exactly where the fixture ended (terminal pick included)."""
     pivots = len(rec["steps"]) - 1
     return pivots if rec["outcome"]["kind"] == "cap" else pivots + 1
+
+
+def check_txt_example(sm_cls, tmp_path, name, device=None):
+    """Write examples.json[name] as the reference UI's .txt, load it through
+    ``sm_cls.from_file`` and compare every get_solution() step with the reference's answer."""
+    from simplex_mi355x import problem_io
+    case = load("examples.json")[name]
+    cons, func = dec_input(case["input"])
+    p = str(tmp_path / f"{name}.txt")
+    # the UI's gradient row carries a third entry (main.py:312 drops it: c = grad[:-1])
+    problem_io.save_txt(p, cons, list(func) + [0.0], 5)
+    got = sm_cls.from_file(p, device=device).get_solution()
+    exp = case["solution"]
+    # the file holds floats: the reference ran integer inputs as ints, which can differ from the
+    # float run only in the sign of a zero (see test_examples_get_solution)
+    ints = any(isinstance(x, int) for r in cons for x in r)
+    assert len(got) == len(exp), name
+    for k, (g, e) in enumerate(zip(got, exp)):
+        if e["kind"] == "error":
+            assert type(g).__name__ == "Error" and str(g) == e["message"], (name, k)
+            continue
+        assert g.row == e["row"] and g.column == e["column"], (name, k)
+        assert (g.i, g.j) == (e["i"], e["j"]), (name, k)
+        assert same_table(g.table, dec_table(e["table"]), signed_zero=not ints), (name, k)
+        for key in ("x1", "x2", "optimum"):
+            assert same_value(getattr(g, key), dec(e[key]), signed_zero=not ints), (name, k, key)

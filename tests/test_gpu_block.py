@@ -289,3 +289,38 @@ def test_deferred_timed_launch_vs_oracle(block_mode):
     got = dev.download()
     assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
     assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
+_NOFREE_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = [{repo!r}, {repo!r} + '/simplex-method-solver_amd', {repo!r} + '/tests']
+import simplex
+from oracle import c_oracle
+from simplex_mi355x import lp
+n = m = 3071
+T = lp.dense_tableau('uniform', 7, n, m)
+sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist(), device='cuda:0')
+assert sm._dev.block_plan() is not None
+sm.solve(record_history=False, max_pivots=24, chunk=12, graph=True)   # captured block graphs
+Tref, st, done, log = c_oracle.run(T, n, m, m, 24, threads=8)
+assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+D = sm._dev.download()
+assert np.array_equal(D[:n].view(np.int64), Tref[:n].view(np.int64))
+print('nofree ok', len(sm._dev._graphs))
+"""
+
+
+def test_nofree_knob_with_captured_block_graph():
+    """SMX_BLK_NOFREE=1 (the A/B knob that turns the sweep's bounded fast path off) set in a fresh
+    process, then block graphs captured: round 2 saw hipError 901 (capture invalidated) here
+    because the knob's device-symbol write ran inside the capture; it now runs in
+    smx_block_bytes, before any capture.  The captured chain stays bit-exact vs the C oracle."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SMX_BLK_NOFREE="1")
+    out = subprocess.run([sys.executable, "-c", _NOFREE_SCRIPT.format(repo=repo)], env=env,
+                         capture_output=True, text=True, timeout=300, cwd=repo)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "nofree ok" in out.stdout

@@ -161,3 +161,41 @@ def test_multi_pick_is_read_only():
     ref = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist(), device="cuda:0")
     ref.solve(record_history=False, max_pivots=4)
     assert ref.pivot_log == sm.pivot_log and table_hash(ref.table) == table_hash(sm.table)
+
+
+@pytest.mark.parametrize("light", [0, 1])
+def test_multi_rccl_exchange_world1_vs_oracle(light):
+    """The branch a real multi-GPU node takes (distinct devices -> exchange="rccl"), run at world
+    size 1: ncclCommInitAll on one device, then per pivot the grouped all-gather of the send
+    slots (full, smx_tune_shard_xchg(0)) or the header all-gather + k_bsh_pick + the grouped
+    int64 MAX all-reduce of the pivot row (light, smx_tune_shard_xchg(1)); smx_mshard_run,
+    reached from SimplexMethod(..., devices=[0], exchange="rccl") as main.py:313 would call it.
+    Pivot log and the whole table bit for bit against the C oracle, then the reference's own
+    example LP through get_solution()."""
+    import simplex
+    from oracle import c_oracle
+    from simplex_mi355x import _lib, lp
+    prev = _lib.tune_shard_xchg(light)
+    try:
+        for kind, n, m, k in (("uniform", 2047, 2047, 41), ("mixed", 1500, 900, 37)):
+            T = lp.dense_tableau(kind, 11, n, m)
+            sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist(), devices=[0],
+                                       exchange="rccl")
+            assert sm.backend == "sharded" and sm._dev.exchange == "rccl"
+            sm.solve(record_history=False, max_pivots=k, chunk=k)
+            Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+            assert sm.pivot_log == [tuple(map(int, x)) for x in log], kind
+            D = sm._dev.download()
+            assert np.array_equal(D[:n].view(np.int64), Tref[:n].view(np.int64)), kind
+            assert np.array_equal(D[n, :m].view(np.int64), Tref[n, :m].view(np.int64)), kind
+            sm._dev.close()
+        case = load("examples.json")["ex2"]
+        cons, func = dec_input(case["input"])
+        sm = simplex.SimplexMethod([list(r) for r in cons], list(func), devices=[0],
+                                   exchange="rccl")
+        got = sm.solve(record_history=False)
+        last = [s for s in case["solution"] if s["kind"] == "info"][-1]
+        assert same_table(got[-1].table, dec_table(last["table"]))
+        sm._dev.close()
+    finally:
+        _lib.tune_shard_xchg(prev)

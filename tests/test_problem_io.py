@@ -61,3 +61,12 @@ def test_smx_rejects_garbage(tmp_path):
     p.write_bytes(b"not a tableau" * 10)
     with pytest.raises(ValueError):
         problem_io.read_header(str(p))
+
+
+@pytest.mark.parametrize("name", list(load("examples.json")))
+def test_from_file_txt_host_engine_vs_reference_examples(tmp_path, name):
+    """The .txt path through the host engine (device="cpu") equals the reference's own
+    get_solution() of every example LP (examples.json); the GPU twin is in test_gpu_parity.py."""
+    import simplex
+    from golden_util import check_txt_example
+    check_txt_example(simplex.SimplexMethod, tmp_path, name, device="cpu")
