@@ -95,13 +95,26 @@ inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     BlkLayout L;
     L.parts = 2 * kBlkHdrBytes;
     L.mul = blk_align(L.parts + (int64_t)kBlkSlots * nparts * 32);
-    L.mul_slot = blk_align(R * kBlkMax * 8);
+    // a plan slot's multipliers [R][kBlkMax], then the sweep's per-row flags int32[R] (blk_rflags)
+    L.mul_slot = blk_align(R * kBlkMax * 8 + R * 4);
     L.pr = L.mul + 2 * L.mul_slot;
     L.pr_slot = blk_align((int64_t)kBlkMax * ld * 8);
     L.fr = L.pr + 2 * L.pr_slot;
-    // then the planner's column cache: [R] "-b" column, [2][R] the next records' column
-    L.bytes = blk_align(L.fr + 2 * ld * 8 + 3 * R * 8);
+    // then the planner's column caches: [R] "-b" column and [2][R] the next records' column of
+    // T_k (pipelined form), [2][R] T_{k+L}[i][cf] and [2][R] T_{k+L}[i][m] (register form)
+    L.bytes = blk_align(L.fr + 2 * ld * 8 + 7 * R * 8);
     return L;
+}
+
+// The sweep's per-row flags of a plan slot (after its R multiplier rows): 1 when the row is no
+// pivot row of the block and every one of its multipliers is bounded (bnd_term < kBndSpan), so
+// blk_sweep_body_flag can take the unchecked fast path on a bounded chunk without re-checking the
+// row's multipliers itself.  Written by the block's last planner step (L == P), f-row included.
+__host__ __device__ __forceinline__ int32_t* blk_rflags(double* mul, int64_t R) {
+    return reinterpret_cast<int32_t*>(mul + R * kBlkMax);
+}
+__host__ __device__ __forceinline__ const int32_t* blk_rflags(const double* mul, int64_t R) {
+    return reinterpret_cast<const int32_t*>(mul + R * kBlkMax);
 }
 
 struct BlkPiv {
@@ -187,11 +200,12 @@ __global__ __launch_bounds__(256) void k_fastdiv_bounded_check(const double* __r
 // `wt` tracks (win_term; a caller recomputes with blk_chain when a wave vote says otherwise,
 // or when a pivot element itself is outside the window).  The planner's chains are latency-
 // bound -- one wave per SIMD, steps in sequence -- so this is what shortens them.
-template <int L>
+// (Q0 > 0: the chain's steps Q0..L-1 only, from x = T_{k+Q0}[i][j])
+template <int L, int Q0 = 0>
 __device__ __forceinline__ double blk_chain_fd(double x, int i, int j, const BlkPiv& pv,
                                                const double* p, const double* mq, uint32_t& wt) {
 #pragma unroll
-    for (int q = 0; q < L; ++q) {
+    for (int q = Q0; q < L; ++q) {
         const double e = pv.e[q];
         // branch-free (the row and column tests differ across lanes): both numerators, then
         // a select -- the pivot row's products are computed and discarded
@@ -209,11 +223,11 @@ __device__ __forceinline__ double blk_chain_fd(double x, int i, int j, const Blk
 
 // T_{k+L}[i][j] from x = T_k[i][j]; p[q] = pr_q[j], mq[q] = mul[i][q] (loaded by the caller, all
 // before the first use, so a chain costs one memory round trip, not L)
-template <int L>
+template <int L, int Q0 = 0>
 __device__ __forceinline__ double blk_chain(double x, int i, int j, const BlkPiv& pv,
                                             const double* p, const double* mq) {
 #pragma unroll
-    for (int q = 0; q < L; ++q) {
+    for (int q = Q0; q < L; ++q) {
         const double e = pv.e[q];
         // branch-free (the row and column tests differ across lanes): both numerators, then
         // a select -- the pivot row's products are computed and discarded
@@ -788,6 +802,11 @@ __device__ __forceinline__ bool blk_step_body(
     if (b == 0 && tid == 0) {
         const FastDiv fd = fd_prep(e);
         mul[(int64_t)rows * kBlkMax + D] = fc;
+        if (L == P) {   // the f-row's sweep flag: never a pivot row; its multipliers are the fc's
+            uint32_t mt = bnd_term(fc);
+            for (int q = 0; q < D; ++q) mt = max(mt, bnd_term(mul[(int64_t)rows * kBlkMax + q]));
+            blk_rflags(mul, rows + 1)[rows] = mt < kBndSpan ? 1 : 0;
+        }
         h->r[D] = r_local;
         h->c[D] = c;
         h->e[D] = e;
@@ -874,18 +893,27 @@ __device__ __forceinline__ bool blk_step_body(
             for (int q = 0; q < L; ++q) blk_pin(colv[k][q]);
         }
     }
+    // Chain-result cache (the register form): step L keeps T_{k+L}[i][m] and T_{k+L}[i][cf] --
+    // the values its records were built on -- in cb / ca by step parity, so step L+1 takes its
+    // multipliers T_{k+L}[i][c] (c = this cf in phase 2) as they are and its "-b" values with ONE
+    // more step, instead of re-deriving both by chains of length L from T_k; only the new
+    // column's chain remains (L+1 chain steps per row instead of 3L-1).  Same operations on the
+    // same operands in the same order as the full chains, so the same bits.  The pipelined (LAG)
+    // form keeps the raw T_k columns (colm, colc) instead.
     double* colm = fr + 2 * ld;
     double* colc = colm + rows;
+    double* cca = colc + 2 * (int64_t)rows;
+    double* ccb = cca + 2 * (int64_t)rows;
     const bool reuse_c = D > 0 && c == s_c;   // phase 2: c is the column of step D's records
     BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
     for (int i = b * NT + tid; i < rows; i += G * NT) {
         const double* row = T + (int64_t)i * ld;
         double* mr = mul + (int64_t)i * kBlkMax;
-        const double xc = reuse_c ? colc[(int64_t)(D & 1) * rows + i] : row[c];
-        const double xb = D > 0 ? colm[i] : row[m];
+        const double xc = reuse_c ? (LAG ? colc : cca)[(int64_t)(D & 1) * rows + i] : row[c];
+        const double xb = D > 0 ? (LAG ? colm[i] : ccb[(int64_t)(D & 1) * rows + i]) : row[m];
         const double xa = cf != SMX_NONE ? row[cf] : 0.0;
-        if (D == 0) colm[i] = xb;
-        if (cf != SMX_NONE) colc[(int64_t)(L & 1) * rows + i] = xa;
+        if (LAG && D == 0) colm[i] = xb;
+        if (LAG && cf != SMX_NONE) colc[(int64_t)(L & 1) * rows + i] = xa;
         double bv, a;
         if constexpr (LAG) {
             // row i's multipliers (previous block's, then this block's) in its LDS operand row
@@ -900,6 +928,15 @@ __device__ __forceinline__ bool blk_step_body(
             const double mc = blk_chain_rolled(xc, i, c, s_all, n, s_colall[0], op);
             mr[D] = mc;                                              // T_{k+D}[i][c]
             op[n] = mc;
+            if (L == P) {   // the sweep's per-row flag (this block's multipliers, blk_rflags)
+                uint32_t mt = bnd_term(mc);
+                bool piv = i == s_all.r[n];
+                for (int q = 0; q < D; ++q) {
+                    mt = max(mt, bnd_term(op[pp + q]));
+                    piv = piv || i == s_all.r[pp + q];
+                }
+                blk_rflags(mul, rows + 1)[i] = (mt < kBndSpan && !piv) ? 1 : 0;
+            }
             bv = blk_chain_rolled(xb, i, m, s_all, n + 1, s_colall[1], op);
             a = cf != SMX_NONE ? blk_chain_rolled(xa, i, cf, s_all, n + 1, s_colall[2], op) : 0.0;
         } else {
@@ -911,16 +948,31 @@ __device__ __forceinline__ bool blk_step_body(
             for (int q = 0; q < D; ++q) blk_pin(mq[q]);
 #pragma unroll
             for (int k = 0; k < 3; ++k) blk_pin(x3[k]);
+            // x3[0]: T_{k+D}[i][c] itself when cached (reuse_c), else T_k[i][c]; x3[1]:
+            // T_{k+D}[i][m] (cached) from step 1 on, T_k[i][m] at step 0
+            constexpr int QB = D > 0 ? D : 0;
             uint32_t wt = 0;
-            mq[D] = blk_chain_fd<D>(x3[0], i, c, pvL, colv[0], mq, wt);   // T_{k+D}[i][c]
-            bv = blk_chain_fd<L>(x3[1], i, m, pvL, colv[1], mq, wt);
+            mq[D] = reuse_c ? x3[0] : blk_chain_fd<D>(x3[0], i, c, pvL, colv[0], mq, wt);
+            bv = blk_chain_fd<L, QB>(x3[1], i, m, pvL, colv[1], mq, wt);
             a = cf != SMX_NONE ? blk_chain_fd<L>(x3[2], i, cf, pvL, colv[2], mq, wt) : 0.0;
             if (!okL || !__all(wt < kWinSpan)) {   // some numerator outside the window
-                mq[D] = blk_chain<D>(x3[0], i, c, pvL, colv[0], mq);
-                bv = blk_chain<L>(x3[1], i, m, pvL, colv[1], mq);
+                if (!reuse_c) mq[D] = blk_chain<D>(x3[0], i, c, pvL, colv[0], mq);
+                bv = blk_chain<L, QB>(x3[1], i, m, pvL, colv[1], mq);
                 a = cf != SMX_NONE ? blk_chain<L>(x3[2], i, cf, pvL, colv[2], mq) : 0.0;
             }
             mr[D] = mq[D];
+            ccb[(int64_t)(L & 1) * rows + i] = bv;
+            if (cf != SMX_NONE) cca[(int64_t)(L & 1) * rows + i] = a;
+            if (L == P) {   // the sweep's per-row flag (blk_rflags)
+                uint32_t mt = 0;
+                bool piv = false;
+#pragma unroll
+                for (int q = 0; q < L; ++q) {
+                    mt = max(mt, bnd_term(mq[q]));
+                    piv = piv || i == pvL.r[q];
+                }
+                blk_rflags(mul, rows + 1)[i] = (mt < kBndSpan && !piv) ? 1 : 0;
+            }
         }
         if (xhist && log_cap > 0) {
             if (i == hl0) xhist[hslot] = bv;
@@ -1511,6 +1563,185 @@ __device__ __forceinline__ void blk_sweep_body_row1(const double* Tin, double* T
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The one-row sweep with the planner's per-row flags (blk_rflags): the unchecked fast path needs a
+// bounded chunk (e and the chunk's pivot-row values in [2^-100, 2^101), checked once per sweep), a
+// flagged row (no pivot row, every multiplier bounded: the planner checked them when it computed
+// them) and bounded inputs (one vote per row).  Re-checking the row's P multipliers in the sweep
+// cost ~30 scalar and ~12 vector instructions per row beside the 120 fp64 ones, and the row's
+// branch waited on them: tools/sweep_lab.hip, 16384^2, P = 10: 894 -> 753 us per sweep
+// (profiles/r03/sweep_lab.jsonl).  The fast path is straight-line: a per-pivot (uniform, never
+// taken) branch to select a pivot column's numerator cost another ~20 % (lab V7 vs V6), so pivot
+// columns are NOT special here.  On a flagged row the pivot column's lane computes
+// RN(x e) - RN(e x) = +0 at its step (its element IS mul[i][q] there) and carries harmless finite
+// values after it; blk_fixcols (k_blk_sweep_rest) then rewrites every pivot column from the planner's multipliers.
+// Rows or chunks outside the fast domain take the window-tracked path (a pivot column's zero
+// numerator fails its vote), then the exact path, which applies every rule itself.
+template <int P, bool NTL>
+__device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* Tout, int64_t ld,
+                                                    int R, int C, const BlkHdr* __restrict__ h,
+                                                    const double* __restrict__ pr,
+                                                    const double* __restrict__ mul) {
+    const int32_t* __restrict__ rfl = blk_rflags(mul, R);
+    const int lane = threadIdx.x & (kWave - 1);
+    int rq[P], cq[P];
+    double eq[P], yq[P];
+    bool allok = true;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        rq[q] = h->r[q];
+        cq[q] = h->c[q];
+        eq[q] = h->e[q];
+        yq[q] = h->y[q];
+        allok = allok && h->ok[q] != 0;
+    }
+    constexpr int kChunk = 2 * kWave;
+    const int NW = (int)gridDim.x * kUpdWaves;
+    const int w = (int)blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nchunks = (C + kChunk - 1) / kChunk;
+    const int qs = NW / nchunks;
+    const int ch = w % nchunks;
+    const int j = ch * kChunk + 2 * lane;
+    dbl2 prs[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+        prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
+                         : dbl2{0.0, 0.0};
+    const bool kNoFree = g_blk_nofree != 0;
+    uint32_t pt = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        pt = max(pt, bnd_term(eq[q]));
+        if (j < C) pt = max(pt, bnd_term(prs[q][0]));
+        if (j + 1 < C) pt = max(pt, bnd_term(prs[q][1]));
+    }
+    const bool chunk_free = !kNoFree && allok && __all(pt < kBndSpan);
+    const int base = w / nchunks;
+    // Every vector load of the loop is this inline asm: a load the compiler can see (the slow
+    // path's reload, as in blk_sweep_body_row1) made it put s_waitcnt vmcnt(0) at the head of the
+    // fast path, waiting for the next row's prefetch before computing this row (sweep 990 us at
+    // P = 10, 16384^2, against 750 us for the lab's loop, tools/sweep_lab.hip).
+    const int jc = min(j, (C - 1) & ~1);
+    auto ldc = [&](int row) {
+        dbl2 v;
+        const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
+        if (NTL)
+            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
+        else
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+        return v;
+    };
+    auto rowf = [&](dbl2 x0, int i0) {
+        const double* m0 = mul + (int64_t)i0 * kBlkMax;
+        double pc0[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) pc0[q] = m0[q];
+        const bool rfree = rfl[i0] != 0;
+        dbl2 v0 = x0;
+        bool ok = false;
+        const uint32_t xt = max((uint32_t)__double2hiint(x0[0]) << 1,
+                                (uint32_t)__double2hiint(x0[1]) << 1);
+        if (chunk_free && rfree && __all(xt < kBndXMax)) {
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const double e = eq[q], y = yq[q];
+                double n[2];
+                n[0] = v0[0] * e - prs[q][0] * pc0[q];
+                n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                double rr[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const double tq = n[k] * y;
+                    const double r = fma(-e, tq, n[k]);
+                    rr[k] = fma(r, y, tq);
+                }
+                v0 = dbl2{rr[0], rr[1]};
+            }
+            ok = true;
+        } else {
+            bool special = !allok;
+#pragma unroll
+            for (int q = 0; q < P; ++q) special = special || i0 == rq[q];
+            if (!special) {
+                // the window-tracked path (numerators checked once per row by a vote)
+                uint32_t wt = 0;
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    const double e = eq[q], y = yq[q];
+                    double n[2];
+                    n[0] = v0[0] * e - prs[q][0] * pc0[q];
+                    n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                    double rr[2];
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        wt = max(wt, win_term(n[k]));
+                        const double tq = n[k] * y;
+                        const double r = fma(-e, tq, n[k]);
+                        rr[k] = fma(r, y, tq);
+                    }
+                    v0 = dbl2{rr[0], rr[1]};
+                }
+                ok = __all(wt < kWinSpan);
+            }
+        }
+        if (!ok) {
+            // reloaded (not written yet, even in place) so x0 need not stay live beside the
+            // fast arithmetic; the wait covers the next row's prefetch too (rare path)
+            x0 = ldc(i0);
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(x0) :: "memory");
+            v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
+        }
+        if (j < C)
+            __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
+    };
+    // prefetch depth 1 over single rows (as blk_sweep_body_row1)
+    dbl2 a = ldc(base), b = ldc(base + qs);
+    asm volatile("s_waitcnt vmcnt(1)" : "+v"(a) :: "memory");
+    for (int i0 = base; i0 < R; i0 += 2 * qs) {
+        rowf(a, i0);
+        if (i0 + qs >= R) break;
+        a = ldc(i0 + 2 * qs);
+        asm volatile("s_waitcnt vmcnt(2)" : "+v"(b) :: "memory");
+        rowf(b, i0 + qs);
+        if (i0 + 2 * qs >= R) break;
+        b = ldc(i0 + 3 * qs);
+        asm volatile("s_waitcnt vmcnt(2)" : "+v"(a) :: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// After a flag-form sweep: every element of every pivot column, rewritten from the planner's
+// multipliers.  For column c whose LAST pivot in the block is q, the element's value before step q
+// is T_{k+q}[i][c] = mul[i][q] (bit for bit, the planner's own chain), so its steps q..P-1 follow
+// from mul alone: step q's numerator is the element itself, or 1.0 on the pivot row
+// (simplex.py:155-160); later steps apply the full rules with the exact division.  Writes `out`,
+// the buffer the sweep wrote.  One (row, pivot) pair per thread, grid-stride.
+__device__ __forceinline__ void blk_fixcols(double* out, int64_t ld, int R, int P,
+                                            const BlkHdr* __restrict__ h,
+                                            const double* __restrict__ mul,
+                                            const double* __restrict__ pr) {
+    const int64_t pairs = (int64_t)R * P;
+    for (int64_t t = (int64_t)blockIdx.x * kUpdBlock + threadIdx.x; t < pairs;
+         t += (int64_t)gridDim.x * kUpdBlock) {
+        const int i = (int)(t / P), q = (int)(t % P);
+        const int c = h->c[q];
+        bool last = true;
+        for (int q2 = q + 1; q2 < P; ++q2) last = last && h->c[q2] != c;
+        if (!last) continue;
+        const double* mr = mul + (int64_t)i * kBlkMax;
+        double x = ((i == h->r[q]) ? 1.0 : mr[q]) / h->e[q];
+        for (int q2 = q + 1; q2 < P; ++q2) {
+            const double e = h->e[q2];
+            double num;
+            if (i == h->r[q2])
+                num = -x;   // c is not pivot q2's column (q is its last pivot)
+            else
+                num = x * e - pr[(int64_t)q2 * ld + c] * mr[q2];
+            x = num / e;
+        }
+        out[(int64_t)i * ld + c] = x;
+    }
+}
+
 // Output: in place when ipx >= 0 and ipx + (pivots applied) is even, else into b_other; the
 // chain state's loc records which buffer (in_idx = index of b_in) now holds the newest table.
 __device__ __forceinline__ double* blk_out(double* b_in, double* b_other, int ipx, int in_idx,
@@ -1535,7 +1766,9 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
                                                          int in_idx) {
     if (h->peff != P) return;
     double* out = blk_out(b_in, b_other, ipx, in_idx, P, hs);
-    if constexpr (FORM == 3)
+    if constexpr (FORM == 4)
+        blk_sweep_body_flag<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
+    else if constexpr (FORM == 3)
         blk_sweep_body_row1<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
     else if constexpr (FORM > 0)
         blk_sweep_body_fixed<P, NTL, (P >= 7), FORM>(b_in, out, ld, R, C, h, pr, mul);
@@ -1543,18 +1776,25 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
         blk_sweep_body<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
 }
 
-// A block that stopped early (a terminal outcome after 0 < peff < P pivots; once per LP): every
-// element through the peff pivots with the exact division, a rolled loop reading each pivot's
-// operands as it goes -- one small kernel for every count instead of a body per count.
-// Launched after k_blk_sweep<P>; does nothing when peff is 0 or P.
+// After k_blk_sweep<P> (one launch, whichever case holds):
+// * fix = 1 and the block applied all P pivots (flag form): blk_fixcols, the pivot columns;
+// * a block that stopped early (a terminal outcome after 0 < peff < P pivots; once per LP):
+//   every element through the peff pivots with the exact division, a rolled loop reading each
+//   pivot's operands as it goes -- one small kernel for every count instead of a body per count;
+// * otherwise nothing.
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep_rest(double* b_in, double* b_other,
                                                               int64_t ld, int R, int C, int P,
                                                               const BlkHdr* __restrict__ h,
                                                               const double* __restrict__ mul,
                                                               const double* __restrict__ pr,
                                                               BlkHdr* __restrict__ hs, int ipx,
-                                                              int in_idx) {
+                                                              int in_idx, int fix, int ipx_full) {
     const int peff = h->peff;
+    if (peff == P && fix) {
+        double* out = (ipx_full >= 0 && ((ipx_full + P) & 1) == 0) ? b_in : b_other;
+        blk_fixcols(out, ld, R, P, h, mul, pr);
+        return;
+    }
     if (peff <= 0 || peff >= P) return;
     double* out = blk_out(b_in, b_other, ipx, in_idx, peff, hs);
     const int64_t half = (C + 1) / 2;   // dbl2 units per row (ld is even)

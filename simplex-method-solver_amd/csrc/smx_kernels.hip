@@ -460,11 +460,13 @@ BlkSweepFn blk_sweep_pick(int P, std::integer_sequence<int, Is...>) {
     return t[P - 1];
 }
 
-// form 0 generic, 1 fixed, 2 fixed with two batches prefetched (streaming loads only)
+// form 0 generic, 1 fixed, 2 fixed with two batches prefetched, 3 one row per batch, 4 one row per
+// batch with the planner's row flags (3 and 4: streaming loads only)
 BlkSweepFn blk_sweep_fn(int P, bool ntl, int form) {
     using All = std::make_integer_sequence<int, kBlkMax>;
     using Low = std::make_integer_sequence<int, 8>;
     if (ntl || P > 8) {
+        if (form == 4) return blk_sweep_pick<true, 4>(P, All{});
         if (form == 3) return blk_sweep_pick<true, 3>(P, All{});
         if (form == 2) return blk_sweep_pick<true, 2>(P, All{});
         return form ? blk_sweep_pick<true, 1>(P, All{}) : blk_sweep_pick<true, 0>(P, All{});
@@ -605,27 +607,45 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
         return e ? atoi(e) : 0;
     }();
     const bool row1 = rows_env == 1 || (rows_env == 0 && P >= 10);
+    // SMX_BLK_FORM (experiments): 1..3 forces an earlier sweep form; default: the flag form (4)
+    static const int form_env = [] {
+        const char* e = getenv("SMX_BLK_FORM");
+        return e ? atoi(e) : 0;
+    }();
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    BlkSweepFn fn = blk_sweep_fn(P, ntl || row1, row1 ? 3 : (P >= 7 ? depth : 1));
+    int form = 4;
+    if (form_env >= 1 && form_env <= 3) form = form_env;
+    if (form == 3 && rows_env == 2) form = P >= 7 ? depth : 1;
+    (void)row1;
+    const bool one_row = form >= 3;
+    BlkSweepFn fn = blk_sweep_fn(P, ntl || one_row, form);
     // the one-row form at P = 10..12 (72-83 VGPRs): 7 blocks per CU, above the occupancy API's
     // 6 / 5 -- 1030-1044 vs 1070-1075 us per 10-pivot sweep and 1189-1196 vs 1234-1255 per
     // 12-pivot sweep at 16384^2 (profiles/r02/sweep_bpc_row1_ab.jsonl; 8 is no better)
-    const int bpc_sweep = bpc_env > 0 ? bpc_env : (row1 && P <= 12 ? 7 : 0);
+    const int bpc_sweep = bpc_env > 0 ? bpc_env : (one_row && P <= 12 ? 7 : 0);
     int grid = update_grid(s, (const void*)fn, 0, bpc_sweep);
     if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
         fn = blk_sweep_fn(P, ntl, 0);
         grid = update_grid(s, (const void*)fn, 0);
+        form = 0;
     }
     BlkHdr* hs = reinterpret_cast<BlkHdr*>(blk);
     const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk + kBlkHdrBytes * slot);
     const double* mul = reinterpret_cast<const double*>(blk + L.mul + slot * L.mul_slot);
     const double* pr = reinterpret_cast<const double*>(blk + L.pr + slot * L.pr_slot);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, tin, tother, s.ld, s.rows + 1,
-                       s.m + 1, h, mul, pr, hs, ipx, in_idx);
-    if (P > 1)   // a block cut short by a terminal outcome (does nothing otherwise)
-        hipLaunchKernelGGL(k_blk_sweep_rest, dim3(num_cus() * 4), dim3(kUpdBlock), 0, st, tin,
+    // SMX_BLK_LDSPAD (experiments): dynamic LDS per sweep workgroup, to cap resident blocks
+    static const int ldspad_env = [] {
+        const char* e = getenv("SMX_BLK_LDSPAD");
+        return e ? atoi(e) : 0;
+    }();
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), (size_t)ldspad_env, st, tin, tother,
+                       s.ld, s.rows + 1, s.m + 1, h, mul, pr, hs, ipx, in_idx);
+    // the flag form's pivot columns, or a block cut short by a terminal outcome (does nothing
+    // otherwise)
+    if (P > 1 || form == 4)
+        hipLaunchKernelGGL(k_blk_sweep_rest, dim3(num_cus() * 2), dim3(kUpdBlock), 0, st, tin,
                            tother, s.ld, s.rows + 1, s.m + 1, P, h, mul, pr, hs, ipx_part,
-                           in_idx);
+                           in_idx, form == 4 ? 1 : 0, ipx);
     return (int)hipGetLastError();
 }
 
