@@ -306,10 +306,13 @@ int smx_resident_run(double* buf0, double* buf1, const smx_shape* shape, int32_t
  * out[1] = pairs whose results differ in any bit (device unsigned long long[2]). */
 int smx_fastdiv_check(const double* num, const double* den, int64_t count,
                       unsigned long long* out, void* stream);
-/* The block sweep's unchecked division (smx_block.hpp, kBndSpan: no per-element window when the
- * pivot elements, pivot-row values and multipliers are bounded) against num / den on the domain
- * those bounds guarantee: den in [2^-100, 2^101), num = +0 or |num| in [2^-254, 2^410).
- * out[0] = pairs inside the domain, out[1] = those that differ in any bit.  Test support. */
+/* The block sweep's unchecked divisions (smx_block.hpp, kBndSpan: no per-element window when the
+ * pivot elements, pivot-row values and multipliers are bounded) against num / den on the domains
+ * those bounds guarantee, den in [2^-100, 2^101): out[0] = pairs with num = +0 or |num| in
+ * [2^-254, 2^410), out[1] = those the hoisted-reciprocal form gets wrong in any bit; out[2] =
+ * pairs with num = +-0 or |num| in [2^-456, 2^410) (zeros allowed), out[3] = those the
+ * zero-safe form (fd_zero: the same plus v_div_fixup_f64) gets wrong.  Device unsigned long
+ * long[4].  Test support. */
 int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t count,
                               unsigned long long* out, void* stream);
 

@@ -106,15 +106,21 @@ inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     return L;
 }
 
-// The sweep's per-row flags of a plan slot (after its R multiplier rows): 1 when the row is no
-// pivot row of the block and every one of its multipliers is bounded (bnd_term < kBndSpan), so
+// The sweep's per-row flags of a plan slot (after its R multiplier rows): 2 for a pivot row of the
+// block, else 1 when every one of the row's multipliers is bounded (bnd_term < kBndSpan), 3 when
+// every one is bounded or an exact +-0 and at least one is zero, 0 otherwise -- so
 // blk_sweep_body_flag can take the unchecked fast path on a bounded chunk without re-checking the
-// row's multipliers itself.  Written by the block's last planner step (L == P), f-row included.
+// row's multipliers, or the pivot rows, itself.  Written by the block's last planner step
+// (L == P), f-row included.
 __host__ __device__ __forceinline__ int32_t* blk_rflags(double* mul, int64_t R) {
     return reinterpret_cast<int32_t*>(mul + R * kBlkMax);
 }
 __host__ __device__ __forceinline__ const int32_t* blk_rflags(const double* mul, int64_t R) {
     return reinterpret_cast<const int32_t*>(mul + R * kBlkMax);
+}
+
+__device__ __forceinline__ int32_t blk_rflag(bool piv, bool bnd, bool zero) {
+    return piv ? 2 : (!bnd ? 0 : (zero ? 3 : 1));
 }
 
 struct BlkPiv {
@@ -167,31 +173,63 @@ constexpr uint32_t kBndXMax = 1124u << 21;         // (hi << 1) below this: |x| 
 __device__ __forceinline__ uint32_t bnd_term(double v) {
     return ((uint32_t)__double2hiint(v) << 1) + kBndBias;
 }
+// bounded or an exact +-0 (the zero-extended domain, fd_zero)
+__device__ __forceinline__ bool bnd_or_zero(double v) {
+    return bnd_term(v) < kBndSpan || (dbits(v) << 1) == 0;
+}
 
-// Self-check of the unchecked sequence on the domain the bounds guarantee (smx_fastdiv_check
+// Zeros in the bounded domain (the flag-form sweep, blk_sweep_body_flag; config 5's integer
+// tables are ~20 % zeros).  Allow pivot-row values, multipliers and input elements to be exact
+// +-0 as well (inputs otherwise in [2^-100, 2^101)).  Where b = RN(p * mq) = +-0 the numerator
+// is RN(x e) -+ 0: +-0 when x is, else RN(x e) itself with |x| bounded below -- an input is
+// >= 2^-100, a chain value after a b != 0 step is >= 2^-254 / 2^101 = 2^-355 (the numerator
+// bound above) and a b = 0 step keeps |x| within a rounding -- so every nonzero numerator lies
+// in [2^-456, 2^410): no scaling case, and the sequence above is exact for it.  A ZERO numerator
+// is the one case it gets wrong: -0 over e > 0 gives +0 (t = -0, r = +0, fma(+0, y, -0) = +0),
+// and every sign-fixed rearrangement fails for one sign of e.  v_div_fixup_f64 -- the last step
+// of the compiler's own division -- returns q unchanged for a finite nonzero numerator, a normal
+// quotient and a normal e, and sign(n) xor sign(e) zero for a zero numerator: one more VALU
+// instruction per element-pivot, paid only on rows or chunks that hold zeros.
+__device__ __forceinline__ double fd_zero(double n, double e, double y) {
+    const double t = n * y;
+    const double r = fma(-e, t, n);
+    return __builtin_amdgcn_div_fixup(fma(r, y, t), e, n);
+}
+
+// Self-check of the unchecked sequences on the domains the bounds guarantee (smx_fastdiv_check
 // bounded): out[0] = pairs with e in [2^-100, 2^101) and num = +0 or |num| in [2^-254, 2^410),
-// out[1] = those whose unchecked quotient differs from num / e in any bit.
+// out[1] = those whose unchecked quotient differs from num / e in any bit; out[2] / out[3] the
+// same for fd_zero on the zero-extended domain (num = +-0 or |num| in [2^-456, 2^410)).
 __global__ __launch_bounds__(256) void k_fastdiv_bounded_check(const double* __restrict__ num,
                                                                const double* __restrict__ den,
                                                                int64_t count,
                                                                unsigned long long* __restrict__ out) {
-    unsigned long long in = 0, bad = 0;
+    unsigned long long in = 0, bad = 0, in2 = 0, bad2 = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count;
          i += (int64_t)gridDim.x * blockDim.x) {
         const double x = num[i], e = den[i];
         const uint32_t xe = ((uint32_t)(dbits(x) >> 52)) & 0x7ffu;
-        const bool dom = bnd_term(e) < kBndSpan &&
-                         (dbits(x) == 0 || (xe >= 1023u - 254u && xe < 1023u + 410u));
-        if (!dom) continue;
-        const FastDiv f = fd_prep(e);
-        const double t = x * f.y;
-        const double r = fma(-e, t, x);
-        const double q = fma(r, f.y, t);
-        ++in;
-        bad += (dbits(q) != dbits(x / e)) ? 1 : 0;
+        if (bnd_term(e) >= kBndSpan) continue;
+        const double ref = x / e;
+        const bool z = (dbits(x) << 1) == 0;
+        if (dbits(x) == 0 || (xe >= 1023u - 254u && xe < 1023u + 410u)) {
+            const FastDiv f = fd_prep(e);
+            const double t = x * f.y;
+            const double r = fma(-e, t, x);
+            const double q = fma(r, f.y, t);
+            ++in;
+            bad += (dbits(q) != dbits(ref)) ? 1 : 0;
+        }
+        if (z || (xe >= 1023u - 456u && xe < 1023u + 410u)) {
+            const double q = fd_zero(x, e, fd_prep(e).y);
+            ++in2;
+            bad2 += (dbits(q) != dbits(ref)) ? 1 : 0;
+        }
     }
     atomicAdd(&out[0], in);
     atomicAdd(&out[1], bad);
+    atomicAdd(&out[2], in2);
+    atomicAdd(&out[3], bad2);
 }
 
 
@@ -803,9 +841,13 @@ __device__ __forceinline__ bool blk_step_body(
         const FastDiv fd = fd_prep(e);
         mul[(int64_t)rows * kBlkMax + D] = fc;
         if (L == P) {   // the f-row's sweep flag: never a pivot row; its multipliers are the fc's
-            uint32_t mt = bnd_term(fc);
-            for (int q = 0; q < D; ++q) mt = max(mt, bnd_term(mul[(int64_t)rows * kBlkMax + q]));
-            blk_rflags(mul, rows + 1)[rows] = mt < kBndSpan ? 1 : 0;
+            bool bnd = bnd_or_zero(fc), zero = (dbits(fc) << 1) == 0;
+            for (int q = 0; q < D; ++q) {
+                const double v = mul[(int64_t)rows * kBlkMax + q];
+                bnd = bnd && bnd_or_zero(v);
+                zero = zero || (dbits(v) << 1) == 0;
+            }
+            blk_rflags(mul, rows + 1)[rows] = blk_rflag(false, bnd, zero);
         }
         h->r[D] = r_local;
         h->c[D] = c;
@@ -929,13 +971,14 @@ __device__ __forceinline__ bool blk_step_body(
             mr[D] = mc;                                              // T_{k+D}[i][c]
             op[n] = mc;
             if (L == P) {   // the sweep's per-row flag (this block's multipliers, blk_rflags)
-                uint32_t mt = bnd_term(mc);
+                bool bnd = bnd_or_zero(mc), zero = (dbits(mc) << 1) == 0;
                 bool piv = i == s_all.r[n];
                 for (int q = 0; q < D; ++q) {
-                    mt = max(mt, bnd_term(op[pp + q]));
+                    bnd = bnd && bnd_or_zero(op[pp + q]);
+                    zero = zero || (dbits(op[pp + q]) << 1) == 0;
                     piv = piv || i == s_all.r[pp + q];
                 }
-                blk_rflags(mul, rows + 1)[i] = (mt < kBndSpan && !piv) ? 1 : 0;
+                blk_rflags(mul, rows + 1)[i] = blk_rflag(piv, bnd, zero);
             }
             bv = blk_chain_rolled(xb, i, m, s_all, n + 1, s_colall[1], op);
             a = cf != SMX_NONE ? blk_chain_rolled(xa, i, cf, s_all, n + 1, s_colall[2], op) : 0.0;
@@ -964,14 +1007,14 @@ __device__ __forceinline__ bool blk_step_body(
             ccb[(int64_t)(L & 1) * rows + i] = bv;
             if (cf != SMX_NONE) cca[(int64_t)(L & 1) * rows + i] = a;
             if (L == P) {   // the sweep's per-row flag (blk_rflags)
-                uint32_t mt = 0;
-                bool piv = false;
+                bool bnd = true, zero = false, piv = false;
 #pragma unroll
                 for (int q = 0; q < L; ++q) {
-                    mt = max(mt, bnd_term(mq[q]));
+                    bnd = bnd && bnd_or_zero(mq[q]);
+                    zero = zero || (dbits(mq[q]) << 1) == 0;
                     piv = piv || i == pvL.r[q];
                 }
-                blk_rflags(mul, rows + 1)[i] = (mt < kBndSpan && !piv) ? 1 : 0;
+                blk_rflags(mul, rows + 1)[i] = blk_rflag(piv, bnd, zero);
             }
         }
         if (xhist && log_cap > 0) {
@@ -1034,6 +1077,31 @@ __device__ __forceinline__ dbl2 blk_exact(dbl2 v, int row, int j, const int* rq,
                 const double a = v[hh] * eq[q];
                 const double b = prs[q][hh] * pc[q];
                 num = (jj == cq[q]) ? v[hh] : (a - b);
+            }
+            v[hh] = num / eq[q];
+        }
+    }
+    return v;
+}
+
+// blk_exact with the pivots' rows and columns read from the header as it goes (the flag form's
+// rare path: no registers held for them across the sweep)
+template <int P>
+__device__ __forceinline__ dbl2 blk_exact_h(dbl2 v, int row, int j, const BlkHdr* __restrict__ h,
+                                            const double* eq, const dbl2* prs, const double* pc) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        const int rq = h->r[q], cq = h->c[q];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int jj = j + hh;
+            double num;
+            if (row == rq) {
+                num = (jj == cq) ? 1.0 : -v[hh];
+            } else {
+                const double a = v[hh] * eq[q];
+                const double b = prs[q][hh] * pc[q];
+                num = (jj == cq) ? v[hh] : (a - b);
             }
             v[hh] = num / eq[q];
         }
@@ -1583,13 +1651,13 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                                                     const double* __restrict__ mul) {
     const int32_t* __restrict__ rfl = blk_rflags(mul, R);
     const int lane = threadIdx.x & (kWave - 1);
-    int rq[P], cq[P];
+    // the pivots' rows and columns are NOT held here: the row flags say which rows are pivot
+    // rows, and only the exact path (blk_exact_h) needs the indices, which it reads from h --
+    // 2P fewer scalar registers (and spills) in the loop
     double eq[P], yq[P];
     bool allok = true;
 #pragma unroll
     for (int q = 0; q < P; ++q) {
-        rq[q] = h->r[q];
-        cq[q] = h->c[q];
         eq[q] = h->e[q];
         yq[q] = h->y[q];
         allok = allok && h->ok[q] != 0;
@@ -1607,14 +1675,23 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
                          : dbl2{0.0, 0.0};
     const bool kNoFree = g_blk_nofree != 0;
-    uint32_t pt = 0;
+    uint32_t et = 0, pt = 0;
+    bool zok = true;   // every pivot-row value bounded or an exact +-0
 #pragma unroll
     for (int q = 0; q < P; ++q) {
-        pt = max(pt, bnd_term(eq[q]));
-        if (j < C) pt = max(pt, bnd_term(prs[q][0]));
-        if (j + 1 < C) pt = max(pt, bnd_term(prs[q][1]));
+        et = max(et, bnd_term(eq[q]));
+        if (j < C) {
+            pt = max(pt, bnd_term(prs[q][0]));
+            zok = zok && bnd_or_zero(prs[q][0]);
+        }
+        if (j + 1 < C) {
+            pt = max(pt, bnd_term(prs[q][1]));
+            zok = zok && bnd_or_zero(prs[q][1]);
+        }
     }
-    const bool chunk_free = !kNoFree && allok && __all(pt < kBndSpan);
+    // chunk_free: bounded, no zeros (fast path); chunk_zok: bounded or zero (zero-safe path)
+    const bool chunk_zok = !kNoFree && allok && et < kBndSpan && __all(zok);
+    const bool chunk_free = chunk_zok && __all(pt < kBndSpan);
     const int base = w / nchunks;
     // Every vector load of the loop is this inline asm: a load the compiler can see (the slow
     // path's reload, as in blk_sweep_body_row1) made it put s_waitcnt vmcnt(0) at the head of the
@@ -1635,12 +1712,17 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         double pc0[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) pc0[q] = m0[q];
-        const bool rfree = rfl[i0] != 0;
+        int rf = rfl[i0];
+        // the row's flag and multipliers in ONE scalar round trip: left alone, the compiler
+        // waits for the flag, branches, and only then issues the multipliers' loads
+#pragma unroll
+        for (int q = 0; q < P; ++q) asm volatile("" : "+s"(pc0[q]));
+        asm volatile("" : "+s"(rf));
         dbl2 v0 = x0;
         bool ok = false;
         const uint32_t xt = max((uint32_t)__double2hiint(x0[0]) << 1,
                                 (uint32_t)__double2hiint(x0[1]) << 1);
-        if (chunk_free && rfree && __all(xt < kBndXMax)) {
+        if (chunk_free && rf == 1 && __all(xt < kBndXMax)) {
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 const double e = eq[q], y = yq[q];
@@ -1657,11 +1739,21 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                 v0 = dbl2{rr[0], rr[1]};
             }
             ok = true;
-        } else {
-            bool special = !allok;
+        } else if (chunk_zok && (rf & 1) && __all(bnd_or_zero(x0[0]) && bnd_or_zero(x0[1]))) {
+            // the zero-extended domain (rf 1 or 3, a chunk or row with exact zeros): the same
+            // arithmetic with fd_zero's v_div_fixup (ONE more instruction per element-pivot)
+            asm volatile("" ::: "memory");   // keeps this path out of the fast path's code
 #pragma unroll
-            for (int q = 0; q < P; ++q) special = special || i0 == rq[q];
-            if (!special) {
+            for (int q = 0; q < P; ++q) {
+                const double e = eq[q], y = yq[q];
+                double n[2];
+                n[0] = v0[0] * e - prs[q][0] * pc0[q];
+                n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                v0 = dbl2{fd_zero(n[0], e, y), fd_zero(n[1], e, y)};
+            }
+            ok = true;
+        } else {
+            if (allok && rf != 2) {   // not a pivot row (rf == 2): the window-tracked path
                 // the window-tracked path (numerators checked once per row by a vote)
                 uint32_t wt = 0;
 #pragma unroll
@@ -1688,7 +1780,7 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
             // fast arithmetic; the wait covers the next row's prefetch too (rare path)
             x0 = ldc(i0);
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(x0) :: "memory");
-            v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
+            v0 = blk_exact_h<P>(x0, i0, j, h, eq, prs, pc0);
         }
         if (j < C)
             __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));

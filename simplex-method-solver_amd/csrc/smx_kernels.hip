@@ -1513,7 +1513,7 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
 int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t count,
                               unsigned long long* out, void* stream) {
     if (count < 0 || !num || !den || !out) return (int)hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), S(stream));
+    hipError_t e = hipMemsetAsync(out, 0, 4 * sizeof(unsigned long long), S(stream));
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_fastdiv_bounded_check, dim3(1024), dim3(256), 0, S(stream), num, den,
                        count, out);

@@ -5,6 +5,8 @@ workgroup count, and interleaved with the host-driven step path.
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import pytest
 
@@ -256,15 +258,25 @@ def test_fastdiv_bounded_domain_matches_hardware_division():
     num = np.concatenate(nums)
     den = np.concatenate(dens)
     num[::97] = 0.0                    # +0 numerators (a zero numerator is never -0 there)
+    # the zero-extended domain of the flag-form sweep (fd_pos): -0 numerators over both signs of
+    # e, the -0.0 values of the edge fixtures, and numerators down to 2^-456
+    edge_zero = [v for rec in load("edge.json").values()
+                 for row in dec_input(rec["input"])[0] for v in row if v == 0.0]
+    assert any(math.copysign(1.0, v) < 0 for v in edge_zero)
+    zn = np.concatenate([np.full(N // 4, -0.0), np.full(N // 4, 0.0), mk(-456, -400),
+                         np.resize(np.array(edge_zero), N // 4)])
+    zd = np.concatenate([mk(-100, 101) for _ in range(4)])[:zn.size]
+    num = np.concatenate([num, zn])
+    den = np.concatenate([den, zd])
     tn = torch.from_numpy(num).cuda()
     td = torch.from_numpy(den).cuda()
-    out = torch.zeros(2, dtype=torch.int64, device="cuda")
+    out = torch.zeros(4, dtype=torch.int64, device="cuda")
     _lib.check(_lib.load().smx_fastdiv_check_bounded(
         tn.data_ptr(), td.data_ptr(), num.size, out.data_ptr(),
         torch.cuda.current_stream().cuda_stream), "smx_fastdiv_check_bounded")
-    inside, bad = (int(x) for x in out.cpu())
-    assert bad == 0
-    assert inside > 0.95 * num.size
+    inside, bad, inside0, bad0 = (int(x) for x in out.cpu())
+    assert bad == 0 and bad0 == 0
+    assert inside > 0.7 * num.size and inside0 > 0.95 * num.size
 
 
 def test_two_resident_chains_on_separate_streams(resident_mode):
