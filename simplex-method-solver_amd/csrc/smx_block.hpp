@@ -1644,6 +1644,13 @@ __device__ __forceinline__ void blk_sweep_body_row1(const double* Tin, double* T
 // values after it; blk_fixcols (k_blk_sweep_rest) then rewrites every pivot column from the planner's multipliers.
 // Rows or chunks outside the fast domain take the window-tracked path (a pivot column's zero
 // numerator fails its vote), then the exact path, which applies every rule itself.
+// SMX_FLAG_FASTONLY: diagnostic build only (tools/sweep_prod_probe.hip): the fast path, then the
+// exact one -- no zero-safe or window-tracked path in the loop
+#ifdef SMX_FLAG_FASTONLY
+constexpr bool kDiagFastOnly = true;
+#else
+constexpr bool kDiagFastOnly = false;
+#endif
 template <int P, bool NTL>
 __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* Tout, int64_t ld,
                                                     int R, int C, const BlkHdr* __restrict__ h,
@@ -1723,12 +1730,21 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         const uint32_t xt = max((uint32_t)__double2hiint(x0[0]) << 1,
                                 (uint32_t)__double2hiint(x0[1]) << 1);
         if (chunk_free && rf == 1 && __all(xt < kBndXMax)) {
+            // the 2P products p * mq first (they do not depend on the chain) and held there:
+            // issued back to back, the chains after them run without waiting on any
+            // (tools/sweep_lab.hip V1: this order, 750-770 us at P = 10, 16384^2; interleaved
+            // with the chains as the compiler otherwise places them, ~850 us)
+            dbl2 bq[P];
+#pragma unroll
+            for (int q = 0; q < P; ++q) bq[q] = dbl2{prs[q][0] * pc0[q], prs[q][1] * pc0[q]};
+#pragma unroll
+            for (int q = 0; q < P; ++q) asm volatile("" : "+v"(bq[q]));
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 const double e = eq[q], y = yq[q];
                 double n[2];
-                n[0] = v0[0] * e - prs[q][0] * pc0[q];
-                n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                n[0] = v0[0] * e - bq[q][0];
+                n[1] = v0[1] * e - bq[q][1];
                 double rr[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
@@ -1739,7 +1755,8 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                 v0 = dbl2{rr[0], rr[1]};
             }
             ok = true;
-        } else if (chunk_zok && (rf & 1) && __all(bnd_or_zero(x0[0]) && bnd_or_zero(x0[1]))) {
+        } else if (!kDiagFastOnly && chunk_zok && (rf & 1) &&
+                   __all(bnd_or_zero(x0[0]) && bnd_or_zero(x0[1]))) {
             // the zero-extended domain (rf 1 or 3, a chunk or row with exact zeros): the same
             // arithmetic with fd_zero's v_div_fixup (ONE more instruction per element-pivot)
             asm volatile("" ::: "memory");   // keeps this path out of the fast path's code
@@ -1752,7 +1769,7 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                 v0 = dbl2{fd_zero(n[0], e, y), fd_zero(n[1], e, y)};
             }
             ok = true;
-        } else {
+        } else if (!kDiagFastOnly) {
             if (allok && rf != 2) {   // not a pivot row (rf == 2): the window-tracked path
                 // the window-tracked path (numerators checked once per row by a vote)
                 uint32_t wt = 0;

@@ -622,7 +622,10 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     // the one-row form at P = 10..12 (72-83 VGPRs): 7 blocks per CU, above the occupancy API's
     // 6 / 5 -- 1030-1044 vs 1070-1075 us per 10-pivot sweep and 1189-1196 vs 1234-1255 per
     // 12-pivot sweep at 16384^2 (profiles/r02/sweep_bpc_row1_ab.jsonl; 8 is no better)
-    const int bpc_sweep = bpc_env > 0 ? bpc_env : (one_row && P <= 12 ? 7 : 0);
+    // the flag form: 5 blocks per CU (all resident at 80 VGPRs), 827-882 vs 855-901 us per
+    // 10-pivot sweep at 16384^2 over 7 (profiles/r03/bpc_ab.jsonl)
+    const int bpc_sweep = bpc_env > 0 ? bpc_env
+                                      : (one_row && P <= 12 ? (form == 4 ? 5 : 7) : 0);
     int grid = update_grid(s, (const void*)fn, 0, bpc_sweep);
     if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
         fn = blk_sweep_fn(P, ntl, 0);

@@ -21,6 +21,8 @@
 //                compiler hoists the two paths' common arithmetic and computes the window terms
 //                on the fast path too (60 extra VALU per row)
 //   V10 (arg 'a') V9 with an empty volatile asm heading the window path, which stops that
+//   V11 (arg 'b') V10 plus a second fast path with v_div_fixup (the production flag form's
+//                zero-safe path) between the fast and the window paths
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off tools/sweep_lab.hip \
 //          -o tools/sweep_lab
@@ -220,10 +222,29 @@ __global__ __launch_bounds__(kBlk) void k_sweep(double* T, int64_t ld, int R, in
                 }
             }
             ok = true;
-        } else if (V == 8 || V == 9 || V == 10) {
+        } else if (V == 11 && __all((((uint32_t)__double2hiint(x0[0]) << 1) + kBndBias < kBndSpan) &&
+                                    (((uint32_t)__double2hiint(x0[1]) << 1) + kBndBias < kBndSpan))) {
+            // V11: a production-like second fast path (v_div_fixup per step) ...
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const double e = eq[q], y = yq[q];
+                const dbl2 p = prs[q];
+                double n[2];
+                n[0] = v[0] * e - p[0] * pc[q];
+                n[1] = v[1] * e - p[1] * pc[q];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const double tq = n[k] * y;
+                    const double r = fma(-e, tq, n[k]);
+                    v[k] = __builtin_amdgcn_div_fixup(fma(r, y, tq), e, n[k]);
+                }
+            }
+            ok = true;
+        } else if (V == 8 || V == 9 || V == 10 || V == 11) {
             // V10: an empty volatile asm first, so the compiler cannot hoist this path's
             // arithmetic (and its window terms) into the common code of both branches
-            if (V == 10) asm volatile("" ::: "memory");
+            if (V == 10 || V == 11) asm volatile("" ::: "memory");
             uint32_t wt = 0;
 #pragma unroll
             for (int q = 0; q < P; ++q) {
@@ -319,7 +340,8 @@ Fn pick(int v) {
         case 7: return k_sweep<P, 7>;
         case 8: return k_sweep<P, 8>;
         case 9: return k_sweep<P, 9>;
-        default: return k_sweep<P, 10>;
+        case 10: return k_sweep<P, 10>;
+        default: return k_sweep<P, 11>;
     }
 }
 Fn pickP(int P, int v) {
@@ -375,7 +397,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e1));
     const double bytes = 16.0 * R * C;
     for (const char* o = only; *o; ++o) {
-        const int v = *o == 'a' ? 10 : *o - '0';
+        const int v = *o == 'a' ? 10 : (*o == 'b' ? 11 : *o - '0');
         Fn fn = pickP(P, v);
         hipFuncAttributes fa;
         CK(hipFuncGetAttributes(&fa, (const void*)fn));
