@@ -779,6 +779,110 @@ __device__ __forceinline__ bool blk_step_body(
     const double* fo = fr + (int64_t)sp * ld;          // f-row of T_{k+D}
     double* fn = fr + (int64_t)(sp ^ 1) * ld;          // f-row of T_{k+L}
     double* prD = pr + (int64_t)D * ld;
+    int c, cf;
+    double e, fc;
+    // Phase 2 of the register form (the benchmark's every step): row r's operands for the pivot
+    // element, the "-b" column, this thread's slice column and its four first-round scan columns
+    // are loaded in ONE round trip, every thread derives e = T_{k+D}[r][c] itself from the
+    // (uniform) operands, and the thread whose scan column is the next entering column hands its
+    // pivot-row value and operands to the row pass through LDS -- three dependent round trips
+    // fewer than the phases below (pivot element, then slice, then scan, then that column).
+    // Same chains on the same operands: the same values.
+    if (!SH && !LAG && nb == SMX_NONE) {
+        c = d.c;
+        const double* Tr = T + (int64_t)r_local * ld;
+        const int S = ((C + G - 1) / G + 1) & ~1;
+        const int s0 = b * S, s1 = min(C, s0 + S);
+        constexpr int NJ = 7;   // c, m, slice, 4 scan columns
+        int jj[NJ];
+        jj[0] = c;
+        jj[1] = m;
+        jj[2] = s0 + tid;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) jj[3 + k] = k * NT + tid;
+        double x[NJ], pq[NJ][kBlkMax], fv[NJ];
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+            const int jc = min(jj[u], C - 1);
+            x[u] = Tr[jc];
+            fv[u] = fo[jc];
+#pragma unroll
+            for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
+        }
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+            blk_pin(x[u]);
+            blk_pin(fv[u]);
+#pragma unroll
+            for (int q = 0; q < D; ++q) blk_pin(pq[u][q]);
+        }
+        double v[NJ];
+        uint32_t wt = 0;
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) v[u] = blk_chain_fd<D>(x[u], r_local, jj[u], pvD, pq[u], mqr, wt);
+        if (!okD || !__all(wt < kWinSpan)) {
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) v[u] = blk_chain<D>(x[u], r_local, jj[u], pvD, pq[u], mqr);
+        }
+        e = v[0];
+        fc = fv[0];
+        SMX_BLK_STAMP(2);
+        // slice b of the pivot row and of the next f-row (columns beyond the first NT: as below)
+        if (jj[2] < s1) {
+            prD[jj[2]] = v[2];
+            fn[jj[2]] = blk_fnew(fv[2], v[2], jj[2], c, e, fc);
+        }
+        for (int j = s0 + tid + NT; j < s1; j += NT) {
+            const double vv = prv(j);
+            prD[j] = vv;
+            fn[j] = blk_fnew(fo[j], vv, j, c, e, fc);
+        }
+        SMX_BLK_STAMP(3);
+        // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
+        int mine = SMX_NONE;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = jj[3 + k];
+            if (j < fscan && blk_fnew(fv[3 + k], v[3 + k], j, c, e, fc) < 0.0 && j < mine) mine = j;
+        }
+        cf = block_min_int<NT>(mine, s_tmp);
+        if (cf != SMX_NONE) {
+            // the owner of column cf: its pivot-row value and operands for the row pass
+            if (tid == cf % NT) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k == cf / NT) {
+                        s_pa = v[3 + k];
+#pragma unroll
+                        for (int q = 0; q < D; ++q) s_col[2][q] = pq[3 + k][q];
+                    }
+            }
+        } else {
+            for (int j0 = kBlkScan; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
+                int mn = SMX_NONE;
+#pragma unroll SCANU
+                for (int k = 0; k < 4; ++k) {
+                    const int j = j0 + k * NT + tid;
+                    if (j < fscan && blk_fnew(fo[j], prv(j), j, c, e, fc) < 0.0 && j < mn) mn = j;
+                }
+                cf = block_min_int<NT>(mn, s_tmp);
+            }
+            if (tid == 0) {
+                s_pa = cf != SMX_NONE ? prv(cf) : 0.0;
+                if (cf != SMX_NONE)
+                    for (int q = 0; q < D; ++q) s_col[2][q] = pr[(int64_t)q * ld + cf];
+            }
+        }
+        if (tid == 0) {
+            s_pm = v[1];
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                s_col[0][q] = pq[0][q];
+                s_col[1][q] = pq[1][q];
+            }
+        }
+        SMX_BLK_STAMP(4);
+    } else {
     if (!SH && nb != SMX_NONE) {
         // phase 1: first j < m with T_{k+D}[r][j] > 0 (simplex.py:81-85), early exit by rounds
         // (sharded: the owner of the row computed it in k_bsh_pack; merge_headers returned it)
@@ -800,7 +904,7 @@ __device__ __forceinline__ bool blk_step_body(
         }
         d.c = p1;
     }
-    const int c = d.c;
+    c = d.c;
     if (tid == 0) {
         s_e = prv(c);
         s_fc = fo[c];
@@ -808,7 +912,8 @@ __device__ __forceinline__ bool blk_step_body(
     }
     __syncthreads();
     SMX_BLK_STAMP(2);
-    const double e = s_e, fc = s_fc;
+    e = s_e;
+    fc = s_fc;
     // slice b of the pivot row and of the next f-row
     {
         const int S = ((C + G - 1) / G + 1) & ~1;
@@ -821,7 +926,7 @@ __device__ __forceinline__ bool blk_step_body(
     }
     SMX_BLK_STAMP(3);
     // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
-    int cf = SMX_NONE;
+    cf = SMX_NONE;
     for (int j0 = 0; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
         int mine = SMX_NONE;
 #pragma unroll SCANU
@@ -833,6 +938,7 @@ __device__ __forceinline__ bool blk_step_body(
     }
     SMX_BLK_STAMP(4);
     if (tid == 0) s_pa = cf != SMX_NONE ? prv(cf) : 0.0;
+    }   // the general path
     // the labels after this pivot (simplex.py:152), identically in every workgroup
     const int hx0 = move_label(ctl->xpos[sp][0], r, c);
     const int hx1 = move_label(ctl->xpos[sp][1], r, c);
@@ -896,6 +1002,7 @@ __device__ __forceinline__ bool blk_step_body(
             if (cf != SMX_NONE) s_colall[2][pp + tid] = pr[(int64_t)tid * ld + cf];
         }
     } else {
+        __syncthreads();   // s_pa / s_pm / s_col of the phase-2 path are written before this
         if (tid == 0) {
             s_pv.r[D] = r_local;
             s_pv.c[D] = c;
@@ -903,7 +1010,7 @@ __device__ __forceinline__ bool blk_step_body(
             s_col[1][D] = s_pm;
             s_col[2][D] = s_pa;
         }
-        if (tid < D) {
+        if (tid < D && !(!SH && nb == SMX_NONE)) {   // (the phase-2 path wrote them already)
             s_col[0][tid] = pr[(int64_t)tid * ld + c];
             s_col[1][tid] = pr[(int64_t)tid * ld + m];
             if (cf != SMX_NONE) s_col[2][tid] = pr[(int64_t)tid * ld + cf];
