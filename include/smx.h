@@ -382,6 +382,14 @@ int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int
                          double* send, double* recv, int32_t nranks, void* comm, int32_t* log,
                          double* xhist, int64_t log_cap, void* stream, float* host_sweep_ms,
                          float* host_total_ms);
+/* smx_bshard_run's chain of k pivots captured as a hipGraph (the RCCL collectives included):
+ * smx_graph_launch replays it with one host call, smx_graph_destroy frees it.  A replay starts
+ * from buf[parity] and leaves the table in buf[(parity + k) & 1]; every rank of the job captures
+ * and replays its own graph in the same order. */
+int smx_bshard_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                            int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                            double* send, double* recv, int32_t nranks, void* comm, int32_t* log,
+                            double* xhist, int64_t log_cap, void* stream, void** graph_out);
 int smx_bshard_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                      void* blk, int64_t blk_bytes, void* stream);
 int smx_bshard_pack(const double* T, const smx_shape* shape, int32_t step, int32_t pivots,

@@ -1655,6 +1655,44 @@ int smx_bshard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t p
                               send, recv, nranks, reinterpret_cast<ncclComm_t>(comm));
 }
 
+// The chain of smx_bshard_run captured once (prime; per block P x [pack -> RCCL exchange ->
+// step], one sweep; publish) -- RCCL collectives are capturable, so one hipGraphLaunch replays
+// the whole per-rank chain and the host enqueues O(1) work per k pivots instead of 3-5 calls per
+// pivot.  The graph is bound to its buffers, comm and parity: a replay starts from
+// buf[parity] and leaves the table in buf[(parity + k) & 1].
+int smx_bshard_graph_create(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
+                            int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
+                            double* send, double* recv, int32_t nranks, void* comm, int32_t* log,
+                            double* xhist, int64_t log_cap, void* stream, void** graph_out) {
+    if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl || !send ||
+        !recv || nranks < 1 || !comm || k < 1 || !graph_out)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = S(stream);
+    Graph* g = new Graph();
+    hipError_t err = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+    if (err != hipSuccess) {
+        delete g;
+        return (int)err;
+    }
+    int lerr = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+                                  static_cast<char*>(blk), log, xhist, log_cap, st, nullptr, send,
+                                  recv, nranks, reinterpret_cast<ncclComm_t>(comm));
+    err = hipStreamEndCapture(st, &g->graph);
+    if (lerr || err != hipSuccess) {
+        if (g->graph) (void)hipGraphDestroy(g->graph);
+        delete g;
+        return lerr ? lerr : (int)err;
+    }
+    err = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+    if (err != hipSuccess) {
+        (void)hipGraphDestroy(g->graph);
+        delete g;
+        return (int)err;
+    }
+    *graph_out = g;
+    return 0;
+}
+
 int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
                          int32_t k, int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes,
                          double* send, double* recv, int32_t nranks, void* comm, int32_t* log,

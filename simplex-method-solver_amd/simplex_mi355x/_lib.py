@@ -68,7 +68,8 @@ EXPORTS = (
     "smx_tune_block", "smx_tune_block_pipe", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
     "smx_block_graph_create",
-    "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_prime",
+    "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_graph_create",
+    "smx_bshard_prime",
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
     "smx_bshard_pick", "smx_bshard_step_light", "smx_tune_shard_xchg",
     "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
@@ -161,6 +162,9 @@ def load():
         "smx_bshard_run_timed": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i32, vp, vp,
                                   vp, i64, vp, ctypes.POINTER(ctypes.c_float),
                                   ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "smx_bshard_graph_create": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i32, vp,
+                                     vp, vp, i64, vp, ctypes.POINTER(ctypes.c_void_p)],
+                                    ctypes.c_int),
         "smx_bshard_prime": ([vp, sp, i32, vp, vp, i64, vp], ctypes.c_int),
         "smx_bshard_pack": ([vp, sp, i32, i32, i32, vp, vp, i64, vp, vp], ctypes.c_int),
         "smx_bshard_step": ([vp, sp, i32, i32, i32, i32, vp, i32, vp, vp, i64, vp, vp, i64,

@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib, lp, ops
-from .device import DeviceTableau
+from .device import DeviceTableau, Graph
 
 
 def row_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -326,6 +326,34 @@ class BlockShardBackend:
         d.step += k
         d._pending = True
 
+    def graph(self, k: int, comm: "RcclComm") -> Graph:
+        """run_native's chain of k pivots captured as a hipGraph (smx_bshard_graph_create), for
+        the current parity; cached per (parity, k, comm)."""
+        d = self.dev
+        key = (d.step & 1, int(k), comm.handle)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        if key not in graphs:
+            h = ctypes.c_void_p()
+            _lib.check(_lib.load().smx_bshard_graph_create(
+                d.buf[0].data_ptr(), d.buf[1].data_ptr(), ctypes.byref(self._shape), d.step & 1,
+                k, self.pivots, d.ctl.data_ptr(), self.blk.data_ptr(), self._nbytes,
+                self.send.data_ptr(), self.recv.data_ptr(), self.world, comm.handle,
+                d.log.data_ptr(), d.xhist.data_ptr(), d.log_cap, d.stream.cuda_stream,
+                ctypes.byref(h)), "smx_bshard_graph_create")
+            graphs[key] = Graph(h.value)
+        return graphs[key]
+
+    def run_graph(self, k: int, comm: "RcclComm") -> None:
+        """run_native(k, comm) as one replay of the captured chain (one host call)."""
+        g = self.graph(k, comm)
+        g.launch(self.dev.stream.cuda_stream)
+        self.dev.step += k
+        self.dev._pending = True
+
+    def drop_graphs(self) -> None:
+        for g in self.__dict__.pop("_graphs", {}).values():
+            g.destroy()
+
     def run_native_timed(self, k: int, comm: "RcclComm"):
         """Like run_native, with HIP events around every sweep (synchronous)."""
         d = self.dev
@@ -422,6 +450,41 @@ class ShardedSolver:
         return self.be.state()
 
 
+def _enqueue_probe(be: BlockShardBackend, comm: "RcclComm", k: int, reps: int = 3) -> dict:
+    """Host enqueue time per pivot of the per-rank chain, eager (smx_bshard_run: prime, per pivot
+    pack + RCCL + step launches, per block a sweep) against one replay of the same chain captured
+    as a hipGraph, next to the device time per pivot (HIP events on the solver stream).  Runs
+    after the timed region (the trajectory continues; every rank issues the same sequence); the
+    median of ``reps`` runs per mode."""
+    st = be.dev.stream
+    out = {"pivots_per_run": k, "runs": reps}
+    with torch.cuda.stream(st):
+        be.graph(k, comm)            # capture for both parities before timing anything
+        if k % 2:
+            be.run_native(k, comm)
+            be.graph(k, comm)
+        torch.cuda.synchronize()
+        for mode in ("eager", "graph"):
+            host, dev = [], []
+            for _ in range(reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                t0 = time.perf_counter()
+                if mode == "eager":
+                    be.run_native(k, comm)
+                else:
+                    be.run_graph(k, comm)
+                host.append(time.perf_counter() - t0)
+                e1.record(st)
+                e1.synchronize()
+                dev.append(e0.elapsed_time(e1) * 1e-3)
+            out[f"{mode}_host_us_per_pivot"] = float(np.median(host)) * 1e6 / k
+            out[f"{mode}_device_us_per_pivot"] = float(np.median(dev)) * 1e6 / k
+    out["npivots_after"] = int(be.state()["npivots"])
+    be.drop_graphs()
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # bench.py --gpus N (launched by torch.distributed.run, one rank per GPU)
 def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
@@ -496,6 +559,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     mn = stats.clone()
     dist.all_reduce(mn, op=dist.ReduceOp.MIN)
     wall = float(mx[0])
+    enqueue = _enqueue_probe(be, comm, args.steps) if block else None
     local_bytes = 16.0 * (hi - lo + 1) * C
     ld = be.dev.ld
     # bytes each rank receives per pivot: full = every rank's slot (8 + 2 ld doubles); light =
@@ -549,6 +613,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
                              (tot_ms - float(upd_ms.sum())) / args.steps},
             "trajectory_valid": bool(mn[2] > 0.5),
             "basis_cycle": cycle,
+            "host_enqueue": enqueue,
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)

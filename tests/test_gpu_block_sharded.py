@@ -214,8 +214,11 @@ def test_block_shards_edge_fixtures(light):
 
 def test_native_block_shard_chain_both_exchanges_vs_oracle():
     """smx_bshard_run with libsmx's own RCCL communicator at world size 1, full and light
-    exchange, against the C oracle (tools/check_native_bshard.py, its own process)."""
+    exchange, eagerly and replayed from captured hipGraphs (smx_bshard_graph_create, RCCL
+    collectives inside the graph), against the C oracle (tools/check_native_bshard.py, its own
+    process)."""
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "check_native_bshard.py")],
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, (out.stdout[-3000:], out.stderr[-3000:])
-    assert out.stdout.count(" ok") == 10, out.stdout
+    assert out.stdout.count(" ok") == 20, out.stdout
+    assert out.stdout.count("graph ") == 10, out.stdout

@@ -28,19 +28,30 @@ for xmode, name in ((0, "full"), (1, "light")):
     _lib.tune_shard_xchg(xmode)
     for kind, n, m, k, P in cases:
         T = lp.dense_tableau(kind, 5, n, m)
-        be = BlockShardBackend(T, n, m, m, 0, 1, device="cuda:0", pivots=P)
-        comm = RcclComm()
-        be.run_native(k, comm)
-        st = be.state()
         Tref, s_ref, done, log = c_oracle.run(T, n, m, m, k, threads=8)
-        got = be.local_table()
-        same = (st["npivots"] == done and np.array_equal(be.log(0, done), log)
-                and np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
-                and (not st["term"] or st["status"] == s_ref))
-        print(name, kind, n, m, P, "pivots", st["npivots"], done,
-              "ok" if same else "MISMATCH", flush=True)
-        ok &= same
-        comm.close()
+        # eager: smx_bshard_run; graph: two replays of captured chains of k // 3 pivots (the
+        # second from the other parity when k // 3 is odd), then the rest eagerly
+        for how in ("eager", "graph"):
+            be = BlockShardBackend(T, n, m, m, 0, 1, device="cuda:0", pivots=P)
+            comm = RcclComm()
+            if how == "eager":
+                be.run_native(k, comm)
+            else:
+                kk = max(1, k // 3)
+                be.run_graph(kk, comm)
+                be.run_graph(kk, comm)
+                if k > 2 * kk:
+                    be.run_native(k - 2 * kk, comm)
+            st = be.state()
+            got = be.local_table()
+            same = (st["npivots"] == done and np.array_equal(be.log(0, done), log)
+                    and np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+                    and (not st["term"] or st["status"] == s_ref))
+            print(name, how, kind, n, m, P, "pivots", st["npivots"], done,
+                  "ok" if same else "MISMATCH", flush=True)
+            ok &= same
+            be.drop_graphs()
+            comm.close()
 _lib.tune_shard_xchg(-1)
 dist.destroy_process_group()
 sys.exit(0 if ok else 1)
