@@ -95,8 +95,9 @@ inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     BlkLayout L;
     L.parts = 2 * kBlkHdrBytes;
     L.mul = blk_align(L.parts + (int64_t)kBlkSlots * nparts * 32);
-    // a plan slot's multipliers [R][kBlkMax], then the sweep's per-row flags int32[R] (blk_rflags)
-    L.mul_slot = blk_align(R * kBlkMax * 8 + R * 4);
+    // a plan slot's multipliers [R][kBlkMax], then the sweep's per-row flags int32[R] (blk_rflags),
+    // then the same multipliers transposed, [kBlkMax][R] (blk_mulT: the planner's row pass)
+    L.mul_slot = blk_align(R * kBlkMax * 8 + blk_align(R * 4) + R * kBlkMax * 8);
     L.pr = L.mul + 2 * L.mul_slot;
     L.pr_slot = blk_align((int64_t)kBlkMax * ld * 8);
     L.fr = L.pr + 2 * L.pr_slot;
@@ -117,6 +118,14 @@ __host__ __device__ __forceinline__ int32_t* blk_rflags(double* mul, int64_t R) 
 }
 __host__ __device__ __forceinline__ const int32_t* blk_rflags(const double* mul, int64_t R) {
     return reinterpret_cast<const int32_t*>(mul + R * kBlkMax);
+}
+
+// The multipliers again, transposed ([q][R], R = rows + 1 as above): the planner's row pass reads
+// mul[i][0..D) of its rows -- one lane per row -- and with the row-major [R][kBlkMax] layout every
+// one of those D loads of a wave touches 64 lines; transposed, each touches 4 (written beside the
+// row-major copy, which the sweep and the pivot-row chains read)
+__host__ __device__ __forceinline__ double* blk_mulT(double* mul, int64_t R) {
+    return mul + R * kBlkMax + (R * 4 + 255) / 256 * 256 / 8;
 }
 
 __device__ __forceinline__ int32_t blk_rflag(bool piv, bool bnd, bool zero) {
@@ -357,6 +366,13 @@ __device__ __forceinline__ double blk_prv(const double* __restrict__ T, int64_t 
     return blk_chain<D>(T[(int64_t)r * ld + j], r, j, pv, p, mqr);
 }
 
+// A lane's double, read by every lane (two v_readlane_b32: the value lands in scalar registers)
+__device__ __forceinline__ double blk_readlane(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
 // The f-row entry after a pivot (row `rows` is never the pivot row): simplex.py:159-160/:166-175
 __device__ __forceinline__ double blk_fnew(double x, double pj, int j, int c, double e,
                                            double fc) {
@@ -423,9 +439,9 @@ __device__ __forceinline__ void blk_rec_store(BlkRec R, smx_part* out) {
     __shared__ First s_f[kBlkNT / kWave];
     __shared__ Cand s_c[kBlkNT / kWave];
     const int tid = threadIdx.x;
-    int nb = wave_min_int(R.nb);
-    First f = wave_first(R.f);
-    Cand bc = wave_best(R.bc);
+    int nb = wave_min_int_dpp(R.nb);
+    First f = wave_first_dpp(R.f);
+    Cand bc = wave_best_dpp(R.bc);
     const int wid = tid >> 6;
     if ((tid & 63) == 0) {
         s_b[wid] = nb;
@@ -504,9 +520,9 @@ __global__ __launch_bounds__(kBlkNT) void k_bsh_pack(
         smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
         const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * nparts;
         if (tid < nparts) rec = slot[tid];
-        const int nb = wave_min_int(rec.p1col);
-        const First f = wave_first(First{rec.first, rec.first_v});
-        const Cand bb = wave_best(Cand{rec.best_cls, rec.best_i, rec.best_v});
+        const int nb = wave_min_int_dpp(rec.p1col);
+        const First f = wave_first_dpp(First{rec.first, rec.first_v});
+        const Cand bb = wave_best_dpp(Cand{rec.best_cls, rec.best_i, rec.best_v});
         if (tid == 0) {
             s_rows[0] = (f.idx != SMX_NONE && isnan(f.v)) ? f.idx - row0 : -1;
             s_rows[1] = (nb != SMX_NONE) ? nb - row0 : (bb.cls < 3 ? bb.idx - row0 : -1);
@@ -548,7 +564,7 @@ __global__ __launch_bounds__(kBlkNT) void k_bsh_pack(
                 const int j = j0 + k * NT + tid;
                 if (j < m && blk_prv<D>(T, ld, rl, j, s_pv, pr, mqr) > 0.0 && j < mine) mine = j;
             }
-            p1 = block_min_int<NT>(mine, s_tmp);
+            p1 = block_min_int_dpp<NT>(mine, s_tmp);
         }
     }
     if (tid == 0) {
@@ -596,12 +612,38 @@ __global__ __launch_bounds__(kUpdBlock) void k_bsh_pick(const double* __restrict
 // 5 row pass operands staged, 6 row pass done, 7 records stored.
 constexpr int kBlkTraceParts = 64;
 __device__ unsigned long long g_blk_trace[kBlkMax + 1][kBlkTraceParts][8];
-#define SMX_BLK_STAMP(ph)                                                              \
+#define SMX_BLK_STAMP_AT(ph)                                                           \
     do {                                                                               \
         if (threadIdx.x == 0 && blockIdx.x < kBlkTraceParts)                           \
             g_blk_trace[L][blockIdx.x][ph] = __builtin_amdgcn_s_memrealtime();         \
     } while (0)
+// waves whose chains left the fast-division window (they recompute with the IEEE division):
+// [L][0] phase-2 pivot-row chains, [L][1] row pass
+__device__ unsigned g_blk_fallback[kBlkMax + 1][2];
+#define SMX_BLK_FALLBACK(k)                                                            \
+    do {                                                                               \
+        if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(&g_blk_fallback[L][k], 1u);    \
+    } while (0)
+#ifdef SMX_BLK_TRACE_P2
+// phase-2 anatomy instead: 2 operands landed, 3 fast chains done, 4 after the exact fallback
+#define SMX_BLK_STAMP(ph) \
+    do {                  \
+        if ((ph) < 2 || (ph) > 4) SMX_BLK_STAMP_AT(ph); \
+    } while (0)
+#define SMX_BLK_STAMP_P2(ph) SMX_BLK_STAMP_AT(ph)
 #else
+#define SMX_BLK_STAMP(ph) SMX_BLK_STAMP_AT(ph)
+#define SMX_BLK_STAMP_P2(ph) \
+    do {                     \
+    } while (0)
+#endif
+#else
+#define SMX_BLK_FALLBACK(k) \
+    do {                    \
+    } while (0)
+#define SMX_BLK_STAMP_P2(ph) \
+    do {                     \
+    } while (0)
 #define SMX_BLK_STAMP(ph) \
     do {                  \
     } while (0)
@@ -649,10 +691,10 @@ __device__ __forceinline__ bool blk_step_body(
     const int b = blockIdx.x, G = gridDim.x;
     SMX_BLK_STAMP(0);
     if (!LAG) pp = 0;
-    if (ctl->term) {
-        if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
-        return true;
-    }
+    // The stop flag is loaded together with the decision's operands and tested after them (one
+    // memory round trip instead of two): on a stopped chain those loads read stale scratch and
+    // their results are discarded.
+    const int stopped = ctl->term;
     const int sp = (parity + D) & 1;   // step parity of block step D
     const int C = m + 1;
     if constexpr (LAG) {
@@ -689,9 +731,9 @@ __device__ __forceinline__ bool blk_step_body(
         const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * G;
         if (tid < G) rec = slot[tid];
         const int c = hs->cfs[blk_slot(D, P, bn)];
-        const int nb = wave_min_int(rec.p1col);
-        const First f = wave_first(First{rec.first, rec.first_v});
-        const Cand bb = wave_best(Cand{rec.best_cls, rec.best_i, rec.best_v});
+        const int nb = wave_min_int_dpp(rec.p1col);
+        const First f = wave_first_dpp(First{rec.first, rec.first_v});
+        const Cand bb = wave_best_dpp(Cand{rec.best_cls, rec.best_i, rec.best_v});
         Decision d;
         d.c = c;
         d.r = SMX_NONE;
@@ -720,6 +762,10 @@ __device__ __forceinline__ bool blk_step_body(
     }
     __syncthreads();
     SMX_BLK_STAMP(1);
+    if (stopped) {
+        if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
+        return true;
+    }
     const int nb = s_nb;
     Decision d = s_d;
     auto terminal = [&](const Decision& dd) {
@@ -782,24 +828,26 @@ __device__ __forceinline__ bool blk_step_body(
     int c, cf;
     double e, fc;
     // Phase 2 of the register form (the benchmark's every step): row r's operands for the pivot
-    // element, the "-b" column, this thread's slice column and its four first-round scan columns
-    // are loaded in ONE round trip, every thread derives e = T_{k+D}[r][c] itself from the
-    // (uniform) operands, and the thread whose scan column is the next entering column hands its
-    // pivot-row value and operands to the row pass through LDS -- three dependent round trips
-    // fewer than the phases below (pivot element, then slice, then scan, then that column).
-    // Same chains on the same operands: the same values.
+    // element, the "-b" column, this thread's slice column and its first-round scan column are
+    // loaded in ONE round trip, and the thread whose scan column is the next entering column hands
+    // its pivot-row value and operands to the row pass through LDS -- three dependent round trips
+    // fewer than the phases below (pivot element, then slice, then scan, then that column).  Three
+    // chains per thread: the two uniform columns are split over the lanes (even lanes c, odd lanes
+    // m; every lane takes e = T_{k+D}[r][c] from lane 0 and T_{k+D}[r][m] from lane 1), and the
+    // first scan round covers the first NT columns (the first negative f-row entry of the
+    // benchmark's LPs lies within the first ~60 columns; wider first rounds cost 4 chains and 4 x
+    // D + 8 loads per thread on every step: tools/trace_planner.hip, profiles/r03/).  Same chains
+    // on the same operands: the same values.
     if (!SH && !LAG && nb == SMX_NONE) {
         c = d.c;
         const double* Tr = T + (int64_t)r_local * ld;
         const int S = ((C + G - 1) / G + 1) & ~1;
         const int s0 = b * S, s1 = min(C, s0 + S);
-        constexpr int NJ = 7;   // c, m, slice, 4 scan columns
+        constexpr int NJ = 3;   // c or m (by lane parity), slice, scan
         int jj[NJ];
-        jj[0] = c;
-        jj[1] = m;
-        jj[2] = s0 + tid;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) jj[3 + k] = k * NT + tid;
+        jj[0] = (tid & 1) ? m : c;
+        jj[1] = s0 + tid;
+        jj[2] = tid;
         double x[NJ], pq[NJ][kBlkMax], fv[NJ];
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
@@ -816,21 +864,28 @@ __device__ __forceinline__ bool blk_step_body(
 #pragma unroll
             for (int q = 0; q < D; ++q) blk_pin(pq[u][q]);
         }
+        SMX_BLK_STAMP_P2(2);
         double v[NJ];
         uint32_t wt = 0;
 #pragma unroll
         for (int u = 0; u < NJ; ++u) v[u] = blk_chain_fd<D>(x[u], r_local, jj[u], pvD, pq[u], mqr, wt);
+#ifdef SMX_BLK_TRACE_P2
+        blk_pin(v[0]);
+#endif
+        SMX_BLK_STAMP_P2(3);
         if (!okD || !__all(wt < kWinSpan)) {
+            SMX_BLK_FALLBACK(0);
 #pragma unroll
             for (int u = 0; u < NJ; ++u) v[u] = blk_chain<D>(x[u], r_local, jj[u], pvD, pq[u], mqr);
         }
-        e = v[0];
-        fc = fv[0];
+        SMX_BLK_STAMP_P2(4);
+        e = blk_readlane(v[0], 0);
+        fc = blk_readlane(fv[0], 0);
         SMX_BLK_STAMP(2);
         // slice b of the pivot row and of the next f-row (columns beyond the first NT: as below)
-        if (jj[2] < s1) {
-            prD[jj[2]] = v[2];
-            fn[jj[2]] = blk_fnew(fv[2], v[2], jj[2], c, e, fc);
+        if (jj[1] < s1) {
+            prD[jj[1]] = v[1];
+            fn[jj[1]] = blk_fnew(fv[1], v[1], jj[1], c, e, fc);
         }
         for (int j = s0 + tid + NT; j < s1; j += NT) {
             const double vv = prv(j);
@@ -839,33 +894,26 @@ __device__ __forceinline__ bool blk_step_body(
         }
         SMX_BLK_STAMP(3);
         // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
-        int mine = SMX_NONE;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int j = jj[3 + k];
-            if (j < fscan && blk_fnew(fv[3 + k], v[3 + k], j, c, e, fc) < 0.0 && j < mine) mine = j;
-        }
-        cf = block_min_int<NT>(mine, s_tmp);
+        const int j2 = jj[2];
+        cf = block_min_int_dpp<NT>(j2 < fscan && blk_fnew(fv[2], v[2], j2, c, e, fc) < 0.0 ? j2
+                                                                                     : SMX_NONE,
+                               s_tmp);
         if (cf != SMX_NONE) {
             // the owner of column cf: its pivot-row value and operands for the row pass
-            if (tid == cf % NT) {
+            if (tid == cf) {
+                s_pa = v[2];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (k == cf / NT) {
-                        s_pa = v[3 + k];
-#pragma unroll
-                        for (int q = 0; q < D; ++q) s_col[2][q] = pq[3 + k][q];
-                    }
+                for (int q = 0; q < D; ++q) s_col[2][q] = pq[2][q];
             }
         } else {
-            for (int j0 = kBlkScan; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
+            for (int j0 = NT; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
                 int mn = SMX_NONE;
 #pragma unroll SCANU
                 for (int k = 0; k < 4; ++k) {
                     const int j = j0 + k * NT + tid;
                     if (j < fscan && blk_fnew(fo[j], prv(j), j, c, e, fc) < 0.0 && j < mn) mn = j;
                 }
-                cf = block_min_int<NT>(mn, s_tmp);
+                cf = block_min_int_dpp<NT>(mn, s_tmp);
             }
             if (tid == 0) {
                 s_pa = cf != SMX_NONE ? prv(cf) : 0.0;
@@ -873,13 +921,10 @@ __device__ __forceinline__ bool blk_step_body(
                     for (int q = 0; q < D; ++q) s_col[2][q] = pr[(int64_t)q * ld + cf];
             }
         }
-        if (tid == 0) {
-            s_pm = v[1];
+        if (tid < 2) {   // lane 0 holds column c's operands, lane 1 column m's
+            if (tid == 1) s_pm = v[0];
 #pragma unroll
-            for (int q = 0; q < D; ++q) {
-                s_col[0][q] = pq[0][q];
-                s_col[1][q] = pq[1][q];
-            }
+            for (int q = 0; q < D; ++q) s_col[tid][q] = pq[0][q];
         }
         SMX_BLK_STAMP(4);
     } else {
@@ -894,7 +939,7 @@ __device__ __forceinline__ bool blk_step_body(
                 const int j = j0 + k * NT + tid;
                 if (j < m && prv(j) > 0.0 && j < mine) mine = j;
             }
-            p1 = block_min_int<NT>(mine, s_tmp);
+            p1 = block_min_int_dpp<NT>(mine, s_tmp);
         }
         if (p1 == SMX_NONE) {
             d.c = SMX_NONE;
@@ -934,7 +979,7 @@ __device__ __forceinline__ bool blk_step_body(
             const int j = j0 + k * NT + tid;
             if (j < fscan && blk_fnew(fo[j], prv(j), j, c, e, fc) < 0.0 && j < mine) mine = j;
         }
-        cf = block_min_int<NT>(mine, s_tmp);
+        cf = block_min_int_dpp<NT>(mine, s_tmp);
     }
     SMX_BLK_STAMP(4);
     if (tid == 0) s_pa = cf != SMX_NONE ? prv(cf) : 0.0;
@@ -1054,6 +1099,7 @@ __device__ __forceinline__ bool blk_step_body(
     double* cca = colc + 2 * (int64_t)rows;
     double* ccb = cca + 2 * (int64_t)rows;
     const bool reuse_c = D > 0 && c == s_c;   // phase 2: c is the column of step D's records
+    double* mT = blk_mulT(mul, rows + 1);
     BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
     for (int i = b * NT + tid; i < rows; i += G * NT) {
         const double* row = T + (int64_t)i * ld;
@@ -1093,7 +1139,7 @@ __device__ __forceinline__ bool blk_step_body(
             double mq[kBlkMax];
             double x3[3] = {xc, xb, xa};
 #pragma unroll
-            for (int q = 0; q < D; ++q) mq[q] = mr[q];
+            for (int q = 0; q < D; ++q) mq[q] = mT[(int64_t)q * (rows + 1) + i];
 #pragma unroll
             for (int q = 0; q < D; ++q) blk_pin(mq[q]);
 #pragma unroll
@@ -1106,11 +1152,13 @@ __device__ __forceinline__ bool blk_step_body(
             bv = blk_chain_fd<L, QB>(x3[1], i, m, pvL, colv[1], mq, wt);
             a = cf != SMX_NONE ? blk_chain_fd<L>(x3[2], i, cf, pvL, colv[2], mq, wt) : 0.0;
             if (!okL || !__all(wt < kWinSpan)) {   // some numerator outside the window
+                SMX_BLK_FALLBACK(1);
                 if (!reuse_c) mq[D] = blk_chain<D>(x3[0], i, c, pvL, colv[0], mq);
                 bv = blk_chain<L, QB>(x3[1], i, m, pvL, colv[1], mq);
                 a = cf != SMX_NONE ? blk_chain<L>(x3[2], i, cf, pvL, colv[2], mq) : 0.0;
             }
             mr[D] = mq[D];
+            mT[(int64_t)D * (rows + 1) + i] = mq[D];
             ccb[(int64_t)(L & 1) * rows + i] = bv;
             if (cf != SMX_NONE) cca[(int64_t)(L & 1) * rows + i] = a;
             if (L == P) {   // the sweep's per-row flag (blk_rflags)
@@ -2052,7 +2100,7 @@ __global__ __launch_bounds__(kWave) void k_blk_publish(const BlkHdr* __restrict_
     const smx_part* sp = parts + (int64_t)slot * nparts;
     int nb = SMX_NONE;
     for (int k = threadIdx.x; k < nparts; k += kWave) nb = min(nb, sp[k].p1col);
-    nb = wave_min_int(nb);
+    nb = wave_min_int_dpp(nb);
     if (threadIdx.x == 0) {
         ctl->negb[parity] = nb;
         ctl->negf[parity] = h->cfs[slot];

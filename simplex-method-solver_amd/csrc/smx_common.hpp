@@ -83,6 +83,87 @@ __device__ __forceinline__ First wave_first(First a) {
     return a;
 }
 
+// The same three reductions through DPP instead of LDS-crossbar shuffles (the planner's per-step
+// decision and record merge, smx_block.hpp): lane pairs within quads (quad_perm), then the
+// half-row and row mirrors (lane i <-> 7 - i, 15 - i) leave every lane of a 16-lane row holding
+// its row's result; the four rows' results are then read from lanes 0 / 16 / 32 / 48 into scalar
+// registers and combined.  Each "take" is a strict total order (ties only between identical
+// values), so any pairing gives the butterfly's result bit for bit.  The whole wave must be active.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+    return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+    return __hiloint2double(dpp_i<CTRL>(__double2hiint(x)), dpp_i<CTRL>(__double2loint(x)));
+}
+__device__ __forceinline__ double readlane_d(double x, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                            __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+constexpr int kDppXor1 = 0xB1;     // quad_perm [1, 0, 3, 2]
+constexpr int kDppXor2 = 0x4E;     // quad_perm [2, 3, 0, 1]
+constexpr int kDppHalfMirror = 0x141;
+constexpr int kDppMirror = 0x140;
+
+__device__ __forceinline__ int wave_min_int_dpp(int x) {
+    x = min(x, dpp_i<kDppXor1>(x));
+    x = min(x, dpp_i<kDppXor2>(x));
+    x = min(x, dpp_i<kDppHalfMirror>(x));
+    x = min(x, dpp_i<kDppMirror>(x));
+    const int a = min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16));
+    const int b = min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48));
+    return min(a, b);
+}
+
+template <int CTRL>
+__device__ __forceinline__ Cand dpp_cand(const Cand& a) {
+    return Cand{dpp_i<CTRL>(a.cls), dpp_i<CTRL>(a.idx), dpp_d<CTRL>(a.v)};
+}
+__device__ __forceinline__ Cand readlane_cand(const Cand& a, int l) {
+    return Cand{__builtin_amdgcn_readlane(a.cls, l), __builtin_amdgcn_readlane(a.idx, l),
+                readlane_d(a.v, l)};
+}
+__device__ __forceinline__ Cand wave_best_dpp(Cand a) {
+    Cand o = dpp_cand<kDppXor1>(a);
+    if (better(o, a)) a = o;
+    o = dpp_cand<kDppXor2>(a);
+    if (better(o, a)) a = o;
+    o = dpp_cand<kDppHalfMirror>(a);
+    if (better(o, a)) a = o;
+    o = dpp_cand<kDppMirror>(a);
+    if (better(o, a)) a = o;
+    Cand r = readlane_cand(a, 0);
+#pragma unroll
+    for (int l = 16; l < kWave; l += 16) {
+        o = readlane_cand(a, l);
+        if (better(o, r)) r = o;
+    }
+    return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ First dpp_first(const First& a) {
+    return First{dpp_i<CTRL>(a.idx), dpp_d<CTRL>(a.v)};
+}
+__device__ __forceinline__ First wave_first_dpp(First a) {
+    First o = dpp_first<kDppXor1>(a);
+    if (o.idx < a.idx) a = o;
+    o = dpp_first<kDppXor2>(a);
+    if (o.idx < a.idx) a = o;
+    o = dpp_first<kDppHalfMirror>(a);
+    if (o.idx < a.idx) a = o;
+    o = dpp_first<kDppMirror>(a);
+    if (o.idx < a.idx) a = o;
+    First r{__builtin_amdgcn_readlane(a.idx, 0), readlane_d(a.v, 0)};
+#pragma unroll
+    for (int l = 16; l < kWave; l += 16) {
+        o = First{__builtin_amdgcn_readlane(a.idx, l), readlane_d(a.v, l)};
+        if (o.idx < r.idx) r = o;
+    }
+    return r;
+}
+
 struct Decision {
     int status;
     int r;

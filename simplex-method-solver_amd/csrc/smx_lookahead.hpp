@@ -26,6 +26,19 @@ __device__ __forceinline__ double nv(const double* __restrict__ T, int64_t ld, i
 }
 
 template <int NT>
+__device__ __forceinline__ int block_min_int_dpp(int x, int* s_tmp) {
+    x = wave_min_int_dpp(x);
+    const int wid = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_tmp[wid] = x;
+    __syncthreads();
+    int r = s_tmp[0];
+#pragma unroll
+    for (int w = 1; w < NT / kWave; ++w) r = min(r, s_tmp[w]);
+    return r;
+}
+
+template <int NT>
 __device__ __forceinline__ int block_min_int(int x, int* s_tmp) {
     x = wave_min_int(x);
     const int wid = threadIdx.x >> 6;

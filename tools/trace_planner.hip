@@ -79,6 +79,12 @@ int main(int argc, char** argv) {
         parity = (parity + P) & 1;
         static unsigned long long tr[kBlkMax + 1][kBlkTraceParts][8];
         CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_blk_trace), sizeof(tr)));
+        static unsigned fb[kBlkMax + 1][2];
+        CK(hipMemcpyFromSymbol(fb, HIP_SYMBOL(g_blk_fallback), sizeof(fb)));
+        {
+            static const unsigned zero[kBlkMax + 1][2] = {};
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_blk_fallback), zero, sizeof(zero)));
+        }
         const int G = s.nparts < kBlkTraceParts ? s.nparts : kBlkTraceParts;
         for (int L = 1; L <= P; ++L) {
             unsigned long long t0 = ~0ull, tend = 0;
@@ -94,7 +100,7 @@ int main(int argc, char** argv) {
                 std::sort(v.begin(), v.end());
                 printf("%s%.2f", ph ? ", " : "", v[v.size() / 2]);
             }
-            printf("]}\n");
+            printf("], \"fallback_waves\": [%u, %u]}\n", fb[L][0], fb[L][1]);
         }
     }
     return 0;
