@@ -58,8 +58,16 @@ struct SmxBool {
 // k_blk_settle moves it to buf[(parity + d) & 1] when a terminal outcome cut the chain.
 constexpr int kBlkMax = 16;          // pivots per block (mul row stride)
 constexpr int kBlkSlots = kBlkMax + 2;   // record / cf slots: steps 1..P-1, and two for step 0
+// Planner workgroups: four waves, one per select partial.  (Tried: one-wave workgroups, four per
+// partial -- the same threads over 256 CUs instead of 64; every workgroup then merges 256 records
+// and the decision phase grew from 2.3-2.8 to 3.7-4.3 us per step: planner 15.2 -> 16.0 us per
+// pivot at 16384^2, profiles/r03b/planner_trace_P10_onewave.jsonl.  The kBlkPartsPer knob keeps
+// that form buildable.)
 constexpr int kBlkNT = kUpdBlock;    // planner workgroup
 constexpr int kBlkScan = 4 * kBlkNT; // columns per early-exit scan round
+constexpr int kBlkPartsPer = kUpdBlock / kBlkNT;
+constexpr int kBlkPartsMax = kMaxParts * kBlkPartsPer;
+__host__ __device__ __forceinline__ int blk_parts_of(int nparts) { return nparts * kBlkPartsPer; }
 
 // One per plan slot (a pipelined chain alternates two); cfs / loc / np0 are the chain's state and
 // live in slot 0 only (`hs` in the kernels).
@@ -466,6 +474,33 @@ __device__ __forceinline__ void blk_rec_store(BlkRec R, smx_part* out) {
     }
 }
 
+// Every lane merges up to kBlkPartsMax / kWave records of a slot (loaded together: one round trip),
+// then the wave reduces them (the order of both merges is immaterial: total orders)
+__device__ __forceinline__ void blk_merge_records(const smx_part* __restrict__ slot, int G,
+                                                  int& nb, First& f, Cand& bb) {
+    constexpr int U = kBlkPartsMax / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    smx_part p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int k = lane + u * kWave;
+        p[u] = k < G ? slot[k] : smx_part{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
+    }
+    int n = SMX_NONE;
+    First fi{SMX_NONE, 0.0};
+    Cand b = cand_none();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        n = min(n, p[u].p1col);
+        if (p[u].first < fi.idx) fi = First{p[u].first, p[u].first_v};
+        const Cand o{p[u].best_cls, p[u].best_i, p[u].best_v};
+        if (better(o, b)) b = o;
+    }
+    nb = wave_min_int_dpp(n);
+    f = wave_first_dpp(fi);
+    bb = wave_best_dpp(b);
+}
+
 // Records of a chain's first step, straight from T (workgroup b of nparts: local rows b*NT + tid
 // + q*nparts*NT, the layout of la_partial; global row indices row0 + i in the records).
 __global__ __launch_bounds__(kBlkNT) void k_blk_first(const double* __restrict__ T, int64_t ld,
@@ -517,12 +552,10 @@ __global__ __launch_bounds__(kBlkNT) void k_bsh_pack(
     if (ctl->term) return;
     blk_load_pivots(h, D, &s_pv);
     if (tid < kWave) {
-        smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
-        const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * nparts;
-        if (tid < nparts) rec = slot[tid];
-        const int nb = wave_min_int_dpp(rec.p1col);
-        const First f = wave_first_dpp(First{rec.first, rec.first_v});
-        const Cand bb = wave_best_dpp(Cand{rec.best_cls, rec.best_i, rec.best_v});
+        int nb;
+        First f;
+        Cand bb;
+        blk_merge_records(parts + (int64_t)blk_slot(D, P, bn) * nparts, nparts, nb, f, bb);
         if (tid == 0) {
             s_rows[0] = (f.idx != SMX_NONE && isnan(f.v)) ? f.idx - row0 : -1;
             s_rows[1] = (nb != SMX_NONE) ? nb - row0 : (bb.cls < 3 ? bb.idx - row0 : -1);
@@ -698,8 +731,8 @@ __device__ __forceinline__ bool blk_step_body(
     const int sp = (parity + D) & 1;   // step parity of block step D
     const int C = m + 1;
     if constexpr (LAG) {
-        if (tid >= kWave && tid - kWave < pp) {
-            const int q = tid - kWave;
+        if (tid < pp) {   // (pp, D <= kBlkMax: lanes of the first wave)
+            const int q = tid;
             s_all.r[q] = hp->r[q];
             s_all.c[q] = hp->c[q];
             s_all.e[q] = hp->e[q];
@@ -727,13 +760,11 @@ __device__ __forceinline__ bool blk_step_body(
         }
     } else if (tid < kWave) {
         // the decision of step D from its records (every workgroup, identically)
-        smx_part rec{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
-        const smx_part* slot = parts + (int64_t)blk_slot(D, P, bn) * G;
-        if (tid < G) rec = slot[tid];
         const int c = hs->cfs[blk_slot(D, P, bn)];
-        const int nb = wave_min_int_dpp(rec.p1col);
-        const First f = wave_first_dpp(First{rec.first, rec.first_v});
-        const Cand bb = wave_best_dpp(Cand{rec.best_cls, rec.best_i, rec.best_v});
+        int nb;
+        First f;
+        Cand bb;
+        blk_merge_records(parts + (int64_t)blk_slot(D, P, bn) * G, G, nb, f, bb);
         Decision d;
         d.c = c;
         d.r = SMX_NONE;
@@ -788,8 +819,7 @@ __device__ __forceinline__ bool blk_step_body(
     const double* prow = SH ? (xrow ? xrow : recv + s_off) : nullptr;   // T_{k+D}[r][*] (sharded)
     double mqr[kBlkMax];
     if constexpr (LAG) {
-        if (tid >= kWave && tid - kWave < pp)
-            s_mrall[tid - kWave] = mulp[(int64_t)r_local * kBlkMax + tid - kWave];
+        if (tid < pp) s_mrall[tid] = mulp[(int64_t)r_local * kBlkMax + tid];
         if (tid < D) s_mrall[pp + tid] = mul[(int64_t)r_local * kBlkMax + tid];
         __syncthreads();
     } else if (!SH) {
@@ -828,26 +858,28 @@ __device__ __forceinline__ bool blk_step_body(
     int c, cf;
     double e, fc;
     // Phase 2 of the register form (the benchmark's every step): row r's operands for the pivot
-    // element, the "-b" column, this thread's slice column and its first-round scan column are
-    // loaded in ONE round trip, and the thread whose scan column is the next entering column hands
-    // its pivot-row value and operands to the row pass through LDS -- three dependent round trips
-    // fewer than the phases below (pivot element, then slice, then scan, then that column).  Three
-    // chains per thread: the two uniform columns are split over the lanes (even lanes c, odd lanes
-    // m; every lane takes e = T_{k+D}[r][c] from lane 0 and T_{k+D}[r][m] from lane 1), and the
-    // first scan round covers the first NT columns (the first negative f-row entry of the
-    // benchmark's LPs lies within the first ~60 columns; wider first rounds cost 4 chains and 4 x
-    // D + 8 loads per thread on every step: tools/trace_planner.hip, profiles/r03/).  Same chains
-    // on the same operands: the same values.
+    // element, the "-b" column, this thread's slice column and its first-round scan column
+    // are loaded in ONE round trip, and the thread whose scan column is the next entering column
+    // hands its pivot-row value and operands to the row pass through LDS -- three dependent round
+    // trips fewer than the phases below (pivot element, then slice, then scan, then that column).
+    // Three chains per thread: the two uniform columns are split over the lanes (even lanes c, odd
+    // lanes m; every lane takes e = T_{k+D}[r][c] from lane 0 and T_{k+D}[r][m] from lane 1), and
+    // the first scan round covers the first NT = 256 columns (the first negative f-row entry of
+    // the benchmark's LPs lies within the first ~60 columns; the earlier first round of 1024
+    // columns cost 7 chains and 7 (D + 2) loads per thread on every step: tools/trace_planner.hip,
+    // profiles/r03b/).  Same chains on the same operands: the same values.
     if (!SH && !LAG && nb == SMX_NONE) {
         c = d.c;
         const double* Tr = T + (int64_t)r_local * ld;
         const int S = ((C + G - 1) / G + 1) & ~1;
         const int s0 = b * S, s1 = min(C, s0 + S);
-        constexpr int NJ = 3;   // c or m (by lane parity), slice, scan
+        constexpr int NSC = NT >= 128 ? 1 : 128 / NT;   // first-round scan columns per thread
+        constexpr int NJ = 2 + NSC;   // c or m (by lane parity), slice, scan columns
         int jj[NJ];
         jj[0] = (tid & 1) ? m : c;
         jj[1] = s0 + tid;
-        jj[2] = tid;
+#pragma unroll
+        for (int k = 0; k < NSC; ++k) jj[2 + k] = tid + k * NT;
         double x[NJ], pq[NJ][kBlkMax], fv[NJ];
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
@@ -894,19 +926,24 @@ __device__ __forceinline__ bool blk_step_body(
         }
         SMX_BLK_STAMP(3);
         // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
-        const int j2 = jj[2];
-        cf = block_min_int_dpp<NT>(j2 < fscan && blk_fnew(fv[2], v[2], j2, c, e, fc) < 0.0 ? j2
-                                                                                     : SMX_NONE,
-                               s_tmp);
+        int mine = SMX_NONE;
+#pragma unroll
+        for (int k = NJ - 1; k >= 2; --k)
+            if (jj[k] < fscan && blk_fnew(fv[k], v[k], jj[k], c, e, fc) < 0.0) mine = jj[k];
+        cf = block_min_int_dpp<NT>(mine, s_tmp);
         if (cf != SMX_NONE) {
             // the owner of column cf: its pivot-row value and operands for the row pass
-            if (tid == cf) {
-                s_pa = v[2];
+            if (tid == cf % NT) {
 #pragma unroll
-                for (int q = 0; q < D; ++q) s_col[2][q] = pq[2][q];
+                for (int k = 2; k < NJ; ++k)
+                    if (k - 2 == cf / NT) {
+                        s_pa = v[k];
+#pragma unroll
+                        for (int q = 0; q < D; ++q) s_col[2][q] = pq[k][q];
+                    }
             }
         } else {
-            for (int j0 = NT; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
+            for (int j0 = NSC * NT; j0 < fscan && cf == SMX_NONE; j0 += kBlkScan) {
                 int mn = SMX_NONE;
 #pragma unroll SCANU
                 for (int k = 0; k < 4; ++k) {
@@ -1035,8 +1072,8 @@ __device__ __forceinline__ bool blk_step_body(
             s_colall[1][n] = s_pm;
             s_colall[2][n] = s_pa;
         }
-        if (tid >= kWave && tid - kWave < pp) {
-            const int q = tid - kWave;
+        if (tid < pp) {
+            const int q = tid;
             s_colall[0][q] = prp[(int64_t)q * ld + c];
             s_colall[1][q] = prp[(int64_t)q * ld + m];
             if (cf != SMX_NONE) s_colall[2][q] = prp[(int64_t)q * ld + cf];

@@ -416,13 +416,14 @@ int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, 
 // Automatic policy from tools/block_bench.py (profiles/r01_block_sweep.jsonl,
 // profiles/r02g_block_pivots.jsonl): below ~48 MiB the planner's ~15 us per pivot eats the saved
 // traffic (2048^2: block 4 = fused within 1 %); 6 pivots per sweep up to 256 MiB (3072^2: 45.8 k
-// pivots/s vs 30.1 k fused), 10 up to 1 GiB (8192^2: 43.4 us per pivot at 10, 44.0 at 8, 43.6 at
-// 12), 12 beyond (16384^2: 125.8 us at 12, 129.5 at 10, 128.0 at 14, 139.3 at 8; the sweep is
-// VALU-bound past ~10 pivots: 0.96 / 1.07 / 1.28 / 1.44 / 1.77 ms at 8 / 10 / 12 / 14 / 16).
+// pivots/s vs 30.1 k fused), 12 beyond (round 2, 16384^2: 125.8 us at 12, 129.5 at 10, 128.0 at
+// 14, 139.3 at 8; the sweep is VALU-bound past ~10 pivots).  Round 3, with the cheaper planner
+// (profiles/r03b/block_pivots_vs_P.jsonl, k = 96): 8192^2 37.8 / 34.2 / 32.0 / 33.6 / 36.1 us per
+// pivot at 8 / 10 / 12 / 14 / 16 (it was 10 up to 1 GiB), 16384^2 109.7 / 101.4 / 98.6 / 104.0 /
+// 100.0 / 109.0 at 10 / 12 / 13 / 14 / 15 / 16.
 int g_block = 0;
 constexpr int64_t kBlockMinTable = 48ll << 20;
 constexpr int64_t kBlockWideTable = 256ll << 20;
-constexpr int64_t kBlockHugeTable = 1ll << 30;
 
 int block_pivots(const smx_shape& s) {
     if (g_block == 1) return 0;
@@ -430,7 +431,7 @@ int block_pivots(const smx_shape& s) {
     if (g_block >= 2) return g_block;
     const int64_t bytes = (int64_t)(s.rows + 1) * s.ld * 8;
     if (bytes < kBlockMinTable) return 0;
-    return bytes >= kBlockHugeTable ? 12 : (bytes >= kBlockWideTable ? 10 : 6);
+    return bytes >= kBlockWideTable ? 12 : 6;
 }
 
 // Pivots of block b when k pivots are cut into ceil(k / P) blocks of near-equal size (the larger
@@ -508,7 +509,7 @@ struct BlkPtrs {
 };
 BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
     BlkPtrs b;
-    b.L = blk_layout(s.rows + 1, s.ld, s.nparts);
+    b.L = blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts));
     for (int k = 0; k < 2; ++k) {
         b.h[k] = reinterpret_cast<BlkHdr*>(blk + kBlkHdrBytes * k);
         b.mul[k] = reinterpret_cast<double*>(blk + b.L.mul + k * b.L.mul_slot);
@@ -524,7 +525,7 @@ int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, s
                      const BlkPtrs& b, hipStream_t st) {
     hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, T, s.ld, s.rows, s.m,
                        fscan_of(s), parity, loc, (const smx_ctl*)ctl, b.h[0], b.h[1], b.fr);
-    hipLaunchKernelGGL(k_blk_first, dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
+    hipLaunchKernelGGL(k_blk_first, dim3(blk_parts_of(s.nparts)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
                        s.row0, (const smx_ctl*)ctl, (const BlkHdr*)b.h[0], b.parts);
     return (int)hipGetLastError();
 }
@@ -538,7 +539,7 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
     BlkStepFn fn = sh ? blk_step_fn_sh<true, false>(L)
                       : (pp > 0 ? blk_step_fn_sh<false, true>(L) : blk_step_fn_sh<false, false>(L));
     const int o = slot ^ 1;
-    hipLaunchKernelGGL(fn, dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
+    hipLaunchKernelGGL(fn, dim3(blk_parts_of(s.nparts)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
                        fscan_of(s), s.row0, P, parity, bn, ctl, b.h[slot], b.h[0], b.parts,
                        b.mul[slot], b.pr[slot], b.fr, recv, nranks, log, xhist, log_cap,
                        (const BlkHdr*)b.h[o], (const double*)b.mul[o], (const double*)b.pr[o],
@@ -565,16 +566,16 @@ int launch_bsh_pick(const double* hdrs, const smx_shape& s, int nranks, int rank
 
 int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
                     const smx_ctl* ctl, const BlkPtrs& b, double* send, hipStream_t st) {
-    hipLaunchKernelGGL(bsh_pack_fn(D), dim3(s.nparts), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
+    hipLaunchKernelGGL(bsh_pack_fn(D), dim3(blk_parts_of(s.nparts)), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
                        s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h[0], (const smx_part*)b.parts,
-                       s.nparts, (const double*)b.mul[0], (const double*)b.pr[0], send);
+                       blk_parts_of(s.nparts), (const double*)b.mul[0], (const double*)b.pr[0], send);
     return (int)hipGetLastError();
 }
 
 int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, const BlkPtrs& b,
                        hipStream_t st) {
     hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)b.h[0],
-                       (const smx_part*)b.parts, s.nparts, blk_slot(0, 1, bn), parity, ctl);
+                       (const smx_part*)b.parts, blk_parts_of(s.nparts), blk_slot(0, 1, bn), parity, ctl);
     return (int)hipGetLastError();
 }
 
@@ -828,7 +829,7 @@ bool block_args_ok(const smx_shape* shape, int k, int P, const void* blk, int64_
     if (!shape_ok(shape) || k < 0 || P < 1 || P > kBlkMax || !blk) return false;
     const smx_shape& s = *shape;
     if (s.row0 != 0 || s.rows != s.n || s.rows < 1 || s.m < 1) return false;
-    return blk_bytes >= blk_layout(s.rows + 1, s.ld, s.nparts).bytes;
+    return blk_bytes >= blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts)).bytes;
 }
 
 // row-sharded blocks: any row block (a rank may own no rows), one f-row replica per rank
@@ -836,7 +837,7 @@ bool bshard_args_ok(const smx_shape* shape, int P, const void* blk, int64_t blk_
     if (!shape_ok(shape) || P < 1 || P > kBlkMax || !blk) return false;
     const smx_shape& s = *shape;
     if (s.rows < 0 || s.n < 1 || s.m < 1 || s.row0 < 0 || s.row0 + s.rows > s.n) return false;
-    return blk_bytes >= blk_layout(s.rows + 1, s.ld, s.nparts).bytes;
+    return blk_bytes >= blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts)).bytes;
 }
 
 struct Graph {
@@ -1550,7 +1551,7 @@ int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout) {
     const int P = req > 0 ? req : block_pivots(*shape);
     if (P < 1 || !block_args_ok(shape, 0, P, shape, INT64_MAX)) return 0;
     if (pivots_inout) *pivots_inout = P;
-    return blk_layout(shape->rows + 1, shape->ld, shape->nparts).bytes;
+    return blk_layout(shape->rows + 1, shape->ld, blk_parts_of(shape->nparts)).bytes;
 }
 
 int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
@@ -1639,7 +1640,7 @@ int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, i
 
 int64_t smx_bshard_bytes(const smx_shape* shape) {
     if (!bshard_args_ok(shape, 1, shape, INT64_MAX)) return 0;
-    return blk_layout(shape->rows + 1, shape->ld, shape->nparts).bytes;
+    return blk_layout(shape->rows + 1, shape->ld, blk_parts_of(shape->nparts)).bytes;
 }
 
 int smx_bshard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
