@@ -1,12 +1,13 @@
 """The committed bench evidence keeps the driver's contract (CPU only: reads profiles/).
 
-profiles/r02/bench_default.json is a `python bench.py --steps 20 --warmup 5` line (the driver's
-command) of this round's GPU run, with its cpu_baseline; profiles/r02/bench_steps200.json and
-kernel_stats_16384_steps200.csv are the bench line and rocprofv3 kernel-trace stats of the same
-command (tools/profile_r02.sh), profiles/r02/pmc/ its FETCH_SIZE / WRITE_SIZE passes.  The
-checks: the JSON line's keys and types, the roofline arithmetic (achieved = algorithmic bytes /
-average launch, frac = achieved / peak), the cpu_baseline block, and that the HIP-event launch
-average agrees with rocprofv3's.
+profiles/r03c/bench20_default.json is a `python bench.py --steps 20 --warmup 5` line (the
+driver's command) of the final round-3 build's GPU run, with its cpu_baseline;
+profiles/r03c/bench_steps{20,200}_rocprof.json and kernel_stats_16384_steps{20,200}.csv are the
+bench lines and rocprofv3 kernel-trace stats of the same commands (tools/profile_r03.sh),
+profiles/r03c/pmc/ the FETCH_SIZE / WRITE_SIZE passes of the --steps 20 line.  The checks: the
+JSON line's keys and types, the roofline arithmetic (achieved = algorithmic bytes / average
+launch, frac = achieved / peak), the cpu_baseline block, and that the HIP-event launch average
+agrees with rocprofv3's.
 """
 import csv
 import json
@@ -35,7 +36,7 @@ def _rocprof_avg_ms(name, needle):
 
 
 def test_default_line_keys():
-    rec = _line("r02/bench_default.json")
+    rec = _line("r03c/bench20_default.json")
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
               "roofline", "cpu_baseline"):
@@ -48,7 +49,7 @@ def test_default_line_keys():
 
 
 def test_roofline_arithmetic():
-    r = _line("r02/bench_default.json")["roofline"]
+    r = _line("r03c/bench20_default.json")["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     ach = r["algorithmic_bytes_per_launch"] / (r["avg_kernel_ms"] * 1e-3) / 1e9
     assert r["achieved"] == pytest.approx(ach, rel=1e-9)
@@ -60,25 +61,38 @@ def test_roofline_arithmetic():
 
 
 def test_cpu_baseline_block():
-    cb = _line("r02/bench_default.json")["cpu_baseline"]
+    cb = _line("r03c/bench20_default.json")["cpu_baseline"]
     assert cb["kind"] in ("port", "reference") and cb["cores"] >= 1
     assert cb["value"] > 0 and cb["unit"] == "pivots/s" and cb["sample"]
 
 
-def test_event_average_agrees_with_rocprof():
-    rec = _line("r02/bench_steps200.json")
+@pytest.mark.parametrize("steps,kernel", [(20, "k_blk_sweep<10>"), (200, "k_blk_sweep<12>")])
+def test_event_average_agrees_with_rocprof(steps, kernel):
+    rec = _line(f"r03c/bench_steps{steps}_rocprof.json")
     r = rec["roofline"]
-    prof = _rocprof_avg_ms("r02/kernel_stats_16384_steps200.csv", "k_blk_sweep<")
-    assert r["kernel"] == "k_blk_sweep<12>"
+    prof = _rocprof_avg_ms(f"r03c/kernel_stats_16384_steps{steps}.csv", "k_blk_sweep<")
+    assert r["kernel"] == kernel
     assert abs(r["avg_kernel_ms"] - prof) / prof < 0.10, (r["avg_kernel_ms"], prof)
 
 
 def test_pmc_summary_matches_csv_passes():
     with open(os.path.join(PROF, "pmc_traffic.json")) as fh:
-        t = json.load(fh)["16384x16384/k_blk_sweep<12>"]
+        t = json.load(fh)["16384x16384/k_blk_sweep<10>"]
     assert t["bytes_per_launch"] == pytest.approx(t["read_bytes_corrected"] + t["write_bytes"])
     assert t["read_bytes_corrected"] == pytest.approx(2 * 1024 * t["fetch_size_kib_median"])
     assert t["write_bytes"] == pytest.approx(1024 * t["write_size_kib_median"])
+    # and it is the median of the committed counter passes
+    import importlib.util
+    import statistics
+    spec = importlib.util.spec_from_file_location(
+        "pmc_traffic", os.path.join(REPO, "tools", "pmc_traffic.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    d = os.path.join(PROF, "r03c", "pmc")
+    assert statistics.median(mod.per_dispatch(d, "FETCH_SIZE", "k_blk_sweep<10")) == \
+        t["fetch_size_kib_median"]
+    assert statistics.median(mod.per_dispatch(d, "WRITE_SIZE", "k_blk_sweep<10")) == \
+        t["write_size_kib_median"]
 
 
 def test_valu_table_matches_counter_summaries():
