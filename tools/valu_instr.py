@@ -12,7 +12,7 @@ import re
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SOURCES = ["profiles/r02d/sweep8_pmc_summary.json",
            "profiles/r03/sweep10_pmc_summary.json",
-           "profiles/r02f/sweep12_pmc_summary.json"]
+           "profiles/r03c/sweep12_pmc_summary.json"]
 SIZE = 16384
 
 
