@@ -408,10 +408,19 @@ __global__ __launch_bounds__(1024) void k_blk_prime(const double* __restrict__ T
     const double* f = T + (int64_t)rows * ld;
     double* fo = fr + (int64_t)parity * ld;
     int nf = SMX_NONE;
-    for (int j = threadIdx.x; j < C; j += 1024) {
-        const double v = f[j];
-        fo[j] = v;
-        if (j < fscan && v < 0.0 && j < nf) nf = j;
+    // eight loads in flight per thread before their stores (one round trip per 8192 columns;
+    // the one-at-a-time loop took ~12 us at 16384 columns)
+    constexpr int U = 8;
+    for (int j0 = threadIdx.x; j0 < C; j0 += 1024 * U) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = j0 + u * 1024 < C ? f[j0 + u * 1024] : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u * 1024;
+            if (j < C) fo[j] = v[u];
+            if (j < fscan && v[u] < 0.0 && j < nf) nf = j;
+        }
     }
     nf = block_min_int<1024>(nf, s_tmp);
     if (threadIdx.x == 0) {
@@ -2020,24 +2029,41 @@ __device__ __forceinline__ void blk_fixcols(double* out, int64_t ld, int R, int 
                                             const BlkHdr* __restrict__ h,
                                             const double* __restrict__ mul,
                                             const double* __restrict__ pr) {
+    // pairs ordered pivot-major (t = q R + i): a wave's lanes share q, so the pivot rows' values
+    // at column c are one address per load; every operand of the chain is loaded before its
+    // first step (the loop that loaded them step by step took 9-13 us per block at 16384^2 --
+    // a memory round trip per step)
     const int64_t pairs = (int64_t)R * P;
     for (int64_t t = (int64_t)blockIdx.x * kUpdBlock + threadIdx.x; t < pairs;
          t += (int64_t)gridDim.x * kUpdBlock) {
-        const int i = (int)(t / P), q = (int)(t % P);
+        const int q = (int)(t / R), i = (int)(t % R);
         const int c = h->c[q];
         bool last = true;
         for (int q2 = q + 1; q2 < P; ++q2) last = last && h->c[q2] != c;
         if (!last) continue;
         const double* mr = mul + (int64_t)i * kBlkMax;
-        double x = ((i == h->r[q]) ? 1.0 : mr[q]) / h->e[q];
-        for (int q2 = q + 1; q2 < P; ++q2) {
-            const double e = h->e[q2];
+        double mq[kBlkMax], pc[kBlkMax], eq[kBlkMax];
+        int rq[kBlkMax];
+#pragma unroll
+        for (int q2 = 0; q2 < kBlkMax; ++q2) {
+            const bool act = q2 >= q && q2 < P;
+            mq[q2] = act ? mr[q2] : 0.0;
+            pc[q2] = (act && q2 > q) ? pr[(int64_t)q2 * ld + c] : 0.0;
+            eq[q2] = act ? h->e[q2] : 1.0;
+            rq[q2] = act ? h->r[q2] : -1;
+        }
+        double x = 0.0;
+#pragma unroll
+        for (int q2 = 0; q2 < kBlkMax; ++q2) {
+            if (q2 < q || q2 >= P) continue;
             double num;
-            if (i == h->r[q2])
+            if (q2 == q)
+                num = (i == rq[q2]) ? 1.0 : mq[q2];
+            else if (i == rq[q2])
                 num = -x;   // c is not pivot q2's column (q is its last pivot)
             else
-                num = x * e - pr[(int64_t)q2 * ld + c] * mr[q2];
-            x = num / e;
+                num = x * eq[q2] - pc[q2] * mq[q2];
+            x = num / eq[q2];
         }
         out[(int64_t)i * ld + c] = x;
     }

@@ -164,6 +164,44 @@ __device__ __forceinline__ First wave_first_dpp(First a) {
     return r;
 }
 
+// Lexicographic (key, row) maximum over the wave by DPP (the resident loop's class-0 ratio:
+// the largest key, ties to the larger row); every lane gets the result.  Whole wave active.
+struct KeyRow {
+    unsigned long long key;
+    int row;
+};
+template <int CTRL>
+__device__ __forceinline__ KeyRow dpp_keyrow(const KeyRow& a) {
+    const unsigned lo = (unsigned)dpp_i<CTRL>((int)(unsigned)a.key);
+    const unsigned hi = (unsigned)dpp_i<CTRL>((int)(unsigned)(a.key >> 32));
+    return KeyRow{((unsigned long long)hi << 32) | lo, dpp_i<CTRL>(a.row)};
+}
+__device__ __forceinline__ bool keyrow_gt(const KeyRow& a, const KeyRow& b) {
+    return a.key > b.key || (a.key == b.key && a.row > b.row);
+}
+__device__ __forceinline__ KeyRow readlane_keyrow(const KeyRow& a, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)a.key, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(a.key >> 32), l);
+    return KeyRow{((unsigned long long)hi << 32) | lo, __builtin_amdgcn_readlane(a.row, l)};
+}
+__device__ __forceinline__ KeyRow wave_max_keyrow_dpp(KeyRow a) {
+    KeyRow o = dpp_keyrow<kDppXor1>(a);
+    if (keyrow_gt(o, a)) a = o;
+    o = dpp_keyrow<kDppXor2>(a);
+    if (keyrow_gt(o, a)) a = o;
+    o = dpp_keyrow<kDppHalfMirror>(a);
+    if (keyrow_gt(o, a)) a = o;
+    o = dpp_keyrow<kDppMirror>(a);
+    if (keyrow_gt(o, a)) a = o;
+    KeyRow r = readlane_keyrow(a, 0);
+#pragma unroll
+    for (int l = 16; l < kWave; l += 16) {
+        o = readlane_keyrow(a, l);
+        if (keyrow_gt(o, r)) r = o;
+    }
+    return r;
+}
+
 struct Decision {
     int status;
     int r;

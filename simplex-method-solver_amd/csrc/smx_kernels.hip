@@ -345,7 +345,7 @@ bool resident_plan(const smx_shape& s, ResPlan* p) {
     p->lds = lds < kResLdsMin ? kResLdsMin : lds;
     p->rec_bytes = (int64_t)2 * G * kResRecWords * 8;
     p->row_off = (p->rec_bytes + 255) / 256 * 256;
-    p->bytes = p->row_off + (int64_t)2 * G * 2 * s.ld * 8;
+    p->bytes = p->row_off + (int64_t)2 * G * 2 * (2 * s.ld) * 8;   // rows as tagged granules
     return true;
 }
 

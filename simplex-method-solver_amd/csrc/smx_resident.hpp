@@ -12,21 +12,23 @@ namespace {
 // MI355X has 256 CUs x 160 KiB of LDS = 40 MiB on chip, so a tableau up to ~2048^2 can stay in
 // LDS for the whole solve: workgroup g (one per CU, 16 waves) owns constraint rows
 // [g*rpw, (g+1)*rpw) and a replica of the f-row; the only per-pivot traffic between CUs is one
-// 32-B record per workgroup and one pivot row.  Per pivot s (T_s in LDS; the entering column cf
-// and the first negative "-b" row lb of T_s were found by the update that produced it):
-//   A  wave 0 builds the record: in phase 1 (lb exists, simplex.py:72-76) the first positive
-//      entry of row lb (:81-85) by ballots; in phase 2 the ratio test on column cf over the local
-//      rows (:105-141) -- first candidate and class masks by ballots, the class-0 maximum by one
-//      LDS atomicMax on an order-preserving key, ties to the larger row;
+// 32-B record per workgroup and one pivot row.  Per pivot s (T_s in LDS):
+//   A  wave 0 finds the entering column cf (first negative f-row entry) and the first local row
+//      lb with a negative "-b" entry by ballots, then builds the record: in phase 1 (lb exists,
+//      simplex.py:72-76) the first positive entry of row lb (:81-85) by ballots; in phase 2 the
+//      ratio test on column cf over the local rows (:105-141) -- first candidate and class masks
+//      by ballots, the class-0 maximum of an order-preserving key (ties to the larger row) by a
+//      DPP (key, row) reduction;
 //   B  wave 0 stores its candidate row(s) (row B: the lb row or the best ratio row; row A: the
-//      first candidate when its ratio is NaN, :117-121) with agent-coherent sc1 stores, waits for
-//      them (s_waitcnt vmcnt(0)) and writes the record as four 8-B {payload, tag} sc1 granules:
-//      the record is its own flag (MI355X_MICROARCH.md "Valid forms", sc1 row 1);
+//      first candidate when its ratio is NaN, :117-121) and its record, all as 8-B {payload, tag}
+//      sc1 granules (a double as two granules of 32-bit halves; the record as four): every
+//      granule is its own flag, so nothing is drained before the record (MI355X_MICROARCH.md,
+//      "R2's granule needs no ordering at all");
 //   C  lanes 0..G-1 poll one record each (sc1 loads) until its tags match, and fold it into LDS
 //      atomics (min first-negative-b row, min first candidate, max class-0 key, min class-1/2
 //      rows); every workgroup reaches the same decision (the arg-min is order-independent);
-//   D  the winning row is staged into LDS with sc1 loads (its producer drained them before
-//      writing the record the poll matched);
+//   D  the winning row is staged into LDS with sc1 loads, each granule's tag checked (a bounded
+//      re-poll if one is still in flight);
 //   E  the Jordan step (:149-177) on the LDS rows in place, flattened over (rows x columns) so
 //      all 16 waves share any shape, with the same per-element expression as k_update (pc
 //      column snapshotted first); ballots over the new f-row and "-b" column give the next
@@ -118,8 +120,6 @@ __global__ __launch_bounds__(256) void k_fastdiv_check(const double* __restrict_
     atomicAdd(&out[1], bad);
 }
 
-// orders one wave's LDS accesses around an LDS atomic (emits s_waitcnt lgkmcnt(0))
-__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
 // One polling wave's reduction of its 64 records (record indices; -1 none; k0 = 0: no class 0,
 // no class-0 key is 0 since that would be a NaN).
@@ -144,7 +144,6 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
     extern __shared__ double s_T[];   // (rpw + 1) rows of ldl, then s_prow[C], then s_pc[rpw + 1]
     __shared__ uint32_t s_rec[kResPollers][kResRecWords];
     __shared__ ResWave s_wred[kResPollers / kWave];
-    __shared__ unsigned long long s_wkey;
     __shared__ int s_err;
     __shared__ int s_cfu;
     constexpr int NT = kResBlock;
@@ -154,6 +153,7 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
     const int g = blockIdx.x;
     const int G = gridDim.x;
     const int C = m + 1;
+    const int64_t ldg = 2 * ldx;              // granules per exchanged row (two per double)
     const int ldl = C | 1;                    // odd LDS stride: column reads spread over banks
     double* s_prow = s_T + (int64_t)(rpw + 1) * ldl;
     double* s_pc = s_prow + C;
@@ -248,7 +248,8 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                     }
                 }
             } else if (cf != SMX_NONE) {   // phase 2: ratio test on column cf (:105-141)
-                unsigned long long lkey = 0;
+                unsigned long long lkey = 0;   // this lane's best class-0 key and its row
+                int lrow = -1;
                 int c1 = SMX_NONE, c2 = SMX_NONE;
                 for (int ib = 0; ib < nl; ib += kWave) {
                     const int i = ib + lane;
@@ -262,30 +263,19 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                         fnan = __shfl(isnan(v) ? 1 : 0, l, kWave) != 0;
                     }
                     const bool nn = cand && !isnan(v);
-                    if (nn && v < 0.0) lkey = max(lkey, key0(v));
+                    if (nn && v < 0.0 && key0(v) >= lkey) {   // rows ascend: ties -> larger row
+                        lkey = key0(v);
+                        lrow = row0 + i;
+                    }
                     const uint64_t m1 = __ballot(nn && v == 0.0), m2 = __ballot(nn && v > 0.0);
                     if (c1 == SMX_NONE && m1) c1 = row0 + ib + __ffsll((long long)m1) - 1;
                     if (c2 == SMX_NONE && m2) c2 = row0 + ib + __ffsll((long long)m2) - 1;
                 }
                 if (__ballot(lkey != 0)) {   // class 0: the largest v, ties to the larger row
-                    if (lane == 0) s_wkey = 0;
-                    wave_lds_fence();
-                    if (lkey) atomicMax(&s_wkey, lkey);
-                    wave_lds_fence();
-                    const unsigned long long kmax = s_wkey;
-                    for (int ib = ((nl - 1) / kWave) * kWave; ib >= 0; ib -= kWave) {
-                        const int i = ib + lane;
-                        const double a = (i < nl) ? s_T[i * ldl + cf] : 0.0;
-                        const double v = (i < nl && a != 0.0) ? s_T[i * ldl + m] / a : 0.0;
-                        const uint64_t mk = __ballot(i < nl && a != 0.0 && v < 0.0 &&
-                                                     key0(v) == kmax);
-                        if (mk) {
-                            const int l = 63 - __clzll((long long)mk);
-                            bidx = row0 + ib + l;
-                            bv = __shfl(v, l, kWave);
-                            break;
-                        }
-                    }
+                    // (key, row) maximum by DPP; v from its key (key0 is a bijection on v < 0)
+                    const KeyRow kr = wave_max_keyrow_dpp(KeyRow{lkey, lrow});
+                    bidx = kr.row;
+                    bv = bitsd(~kr.key);
                     bcls = 0;
                 } else if (c1 != SMX_NONE) {
                     bcls = 1;
@@ -300,27 +290,32 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
             if (s < k) {
                 const int rb = (lb != SMX_NONE) ? lb : (bcls < 2 ? bidx : -1);
                 const int ra = (lb == SMX_NONE && fidx != SMX_NONE && fnan) ? fidx : -1;
-                uint64_t* dst = xrow + ((int64_t)slot * G + g) * 2 * ldx;
-                // eight LDS reads in flight, then eight sc1 stores
+                uint64_t* dst = xrow + ((int64_t)slot * G + g) * 2 * ldg;
+                // the candidate rows as tagged granules: each double as two {32-bit half, tag}
+                // sc1 stores, so the record below needs no drain of these stores before it (the
+                // reader checks every granule's tag; the drain cost ~1 us per pivot at 1024^2).
+                // Four LDS reads in flight, then eight sc1 stores
                 auto put = [&](uint64_t* d, int il) {
-                    for (int jb = 0; jb < C; jb += 8 * kWave) {
-                        uint64_t v[8];
+                    for (int jb = 0; jb < C; jb += 4 * kWave) {
+                        uint64_t v[4];
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) {
+                        for (int u = 0; u < 4; ++u) {
                             const int j = jb + u * kWave + lane;
                             v[u] = j < C ? dbits(s_T[il * ldl + j]) : 0;
                         }
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) {
+                        for (int u = 0; u < 4; ++u) {
                             const int j = jb + u * kWave + lane;
-                            if (j < C) st_sc1(d + j, v[u]);
+                            if (j < C) {
+                                st_sc1(d + 2 * j, tag | (uint32_t)v[u]);
+                                st_sc1(d + 2 * j + 1, tag | (uint32_t)(v[u] >> 32));
+                            }
                         }
                     }
                 };
-                if (rb >= 0) put(dst + ldx, rb - row0);
+                if (rb >= 0) put(dst + ldg, rb - row0);
                 if (ra >= 0) put(dst, ra - row0);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) {
                 uint64_t* rec = xrec + ((int64_t)slot * G + g) * kResRecWords;
                 const uint32_t w0 = (lb == SMX_NONE ? 0xffffu : (uint32_t)lb) |
@@ -438,8 +433,24 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
 
         // ---- D: stage the pivot row, snapshot column c, bookkeeping ----------------------------
         const int r = d.r, c = d.c;
-        const uint64_t* src = xrow + (((int64_t)slot * G + d.owner) * 2 + d.rowsel) * ldx;
-        for (int j = tid; j < C; j += NT) s_prow[j] = bitsd(ld_sc1(src + j));
+        const uint64_t* src = xrow + (((int64_t)slot * G + d.owner) * 2 + d.rowsel) * ldg;
+        for (int j = tid; j < C; j += NT) {
+            uint64_t lo = ld_sc1(src + 2 * j), hi = ld_sc1(src + 2 * j + 1);
+            if ((uint32_t)(lo >> 32) != want || (uint32_t)(hi >> 32) != want) {
+                const int64_t t0 = rt_now();
+                for (;;) {   // a granule still in flight (bounded like every spin)
+                    __builtin_amdgcn_s_sleep(1);
+                    lo = ld_sc1(src + 2 * j);
+                    hi = ld_sc1(src + 2 * j + 1);
+                    if ((uint32_t)(lo >> 32) == want && (uint32_t)(hi >> 32) == want) break;
+                    if (rt_now() - t0 > g_res_spin_ticks || *(volatile int*)&s_err) {
+                        s_err = 1;
+                        break;
+                    }
+                }
+            }
+            s_prow[j] = bitsd((lo & 0xffffffffull) | (hi << 32));
+        }
         for (int i = tid; i <= rpw; i += NT)
             if (i < nl || i == fl) s_pc[i] = s_T[i * ldl + c];
         const int64_t kk = npiv0 + s;
@@ -452,6 +463,7 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
         xp0 = move_label(xp0, r, c);   // label swap (simplex.py:152)
         xp1 = move_label(xp1, r, c);
         __syncthreads();
+        if (s_err) break;
         stamp(s, 4);
         const double e = s_prow[c];
         last_r = r;
