@@ -420,7 +420,9 @@ int launch_resident(double* buf0, double* buf1, const smx_shape& s, int parity, 
 // 14, 139.3 at 8; the sweep is VALU-bound past ~10 pivots).  Round 3, with the cheaper planner
 // (profiles/r03b/block_pivots_vs_P.jsonl, k = 96): 8192^2 37.8 / 34.2 / 32.0 / 33.6 / 36.1 us per
 // pivot at 8 / 10 / 12 / 14 / 16 (it was 10 up to 1 GiB), 16384^2 109.7 / 101.4 / 98.6 / 104.0 /
-// 100.0 / 109.0 at 10 / 12 / 13 / 14 / 15 / 16.
+// 100.0 / 109.0 at 10 / 12 / 13 / 14 / 15 / 16; 48-256 MiB now 10 (it was 6;
+// profiles/r03d/block_pivots_mid_sizes.jsonl: 3072^2 17.0 / 15.7 / 15.8 us per pivot at 6 / 8 /
+// 10, 4096^2 20.4 / 18.3 / 18.0).
 int g_block = 0;
 constexpr int64_t kBlockMinTable = 48ll << 20;
 constexpr int64_t kBlockWideTable = 256ll << 20;
@@ -431,7 +433,7 @@ int block_pivots(const smx_shape& s) {
     if (g_block >= 2) return g_block;
     const int64_t bytes = (int64_t)(s.rows + 1) * s.ld * 8;
     if (bytes < kBlockMinTable) return 0;
-    return bytes >= kBlockWideTable ? 12 : 6;
+    return bytes >= kBlockWideTable ? 12 : 10;
 }
 
 // Pivots of block b when k pivots are cut into ceil(k / P) blocks of near-equal size (the larger

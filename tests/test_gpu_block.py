@@ -221,10 +221,10 @@ def test_block_terminal_state_matches_chain(block_mode):
 
 
 @pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 23, 12), (16383, 16383, 9, 12),
-                                     (16383, 16383, 20, 12), (3071, 3071, 13, 6)])
+                                     (16383, 16383, 20, 12), (3071, 3071, 13, 10)])
 def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
-    """BASELINE sizes through the default policy (6 or 12 pivots per sweep at most, blocks of
-    near-equal size: 23 = 12 + 11, 9 = one block, 20 = 10 + 10, 13 = 5 + 4 + 4)."""
+    """BASELINE sizes through the default policy (10 or 12 pivots per sweep at most, blocks of
+    near-equal size: 23 = 12 + 11, 9 = one block, 20 = 10 + 10, 13 = 7 + 6)."""
     from simplex_mi355x import lp, _lib
     from simplex_mi355x.device import DeviceTableau
     from oracle import c_oracle
@@ -247,7 +247,7 @@ def test_block_plan_policy(block_mode):
     block_mode(0)
     assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 12
     assert _lib.block_plan([8192, 8191, 8191, 8191, 8191, 0, 32])[1] == 12
-    assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 6
+    assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 10
     assert _lib.block_plan([2048, 2047, 2047, 2047, 2047, 0, 8]) is None    # below 48 MiB
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4]) is None
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 6)[1] == 6
