@@ -45,6 +45,33 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 PEAK_CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
+L2_AGG_GBS = 36900.0   # aggregate L2 read rate, 8 XCDs (MI355X_MICROARCH.md, L2 section)
+MALL_BYTES = 256 << 20  # Infinity Cache: a working set beyond it streams from HBM
+
+
+def physical_limit_gbs(footprint_bytes):
+    """The fastest rate any kernel can move bytes over a working set of `footprint_bytes`:
+    HBM peak (8 TB/s) beyond the Infinity Cache, the aggregate L2 rate within it."""
+    return PEAK_HBM_GBS if footprint_bytes > MALL_BYTES else L2_AGG_GBS
+
+
+def physical_check(name, bytes_per_launch, seconds_per_launch, footprint_bytes):
+    """Refuse a measurement whose implied rate (bytes one launch moves / its duration) exceeds
+    what the memory system can deliver: a kernel that did no work, a graph that captured nothing
+    or events that bracket the wrong stream all show up here.  Returns the rate in GB/s; raises
+    ValueError for an impossible one."""
+    if not seconds_per_launch > 0.0:
+        raise ValueError(f"{name}: non-positive launch time {seconds_per_launch!r}")
+    gbs = bytes_per_launch / seconds_per_launch / 1e9
+    lim = physical_limit_gbs(footprint_bytes)
+    if gbs > lim:
+        raise ValueError(f"{name}: {bytes_per_launch:.4g} B in {seconds_per_launch * 1e6:.4g} us "
+                         f"= {gbs:.0f} GB/s exceeds the physical limit {lim:.0f} GB/s for a "
+                         f"{footprint_bytes / 2**20:.1f} MiB working set: the measurement is "
+                         f"broken (no work done, or the wrong stream timed)")
+    return gbs
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -254,7 +281,7 @@ def _single_pivot_line(dev, R, C, k):
         dev.sync_state()
     finally:
         dev.block = prev_block
-    ach = 16.0 * R * C / (ms * 1e-3 / k) / 1e9
+    ach = physical_check("single_pivot_update", 16.0 * R * C, ms * 1e-3 / k, 16.0 * R * C)
     return {"kernel": "k_update<kFused>", "pivots_per_launch": 1, "pivots": k,
             "pivots_s": k / ms * 1e3, "avg_kernel_ms": ms / k, "achieved": ach,
             "unit": "GB/s", "frac": ach / PEAK_HBM_GBS}
@@ -344,8 +371,15 @@ def run_single(args):
     done = int(ctl["npivots"])
     valid = done == args.warmup + args.steps and not ctl["term"]
     cycle = cycle_report(n, m, dev.read_log(0, done))
-    achieved = bytes_per_sweep / avg_kernel / 1e9
-    workload = f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
+    if resident is not None:
+        # algorithmic bytes of a chain held in LDS: not an HBM rate, no physical bound applies
+        achieved = bytes_per_sweep / avg_kernel / 1e9
+    else:
+        # the sweep / update moves every element in and out once per launch; an in-place sweep's
+        # working set is one buffer (8 B per element), so that is the footprint that decides
+        # whether HBM or the caches bound it
+        achieved = physical_check(kernel, bytes_per_sweep, avg_kernel, 8.0 * R * C)
+    workload =f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
     copy_gbs = copy_ceiling(8.0 * R * C)   # same bytes as one sweep (outside timing)
     single = None
     if bplan is not None and valid:

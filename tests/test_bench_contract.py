@@ -134,3 +134,63 @@ def test_two_term_arithmetic(monkeypatch):
     assert t["hbm_peak_ms"] == pytest.approx(t_hbm * 1e3)
     assert t["bound"] == "valu" and t["frac"] == pytest.approx(max(t_valu, t_hbm) / 1.2e-3)
     assert bench.two_term(R, C, 4, 8.15, 1.0e-3, hbm)["bound"] == "hbm"
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def test_physical_guard_rejects_impossible_rates():
+    """bench.physical_check refuses a launch that would move bytes faster than the memory system
+    can (the round-3 forced-update record: 1.07 GB in 0.26 us); accepts the real ones."""
+    bench = _bench_module()
+    R = 8192
+    b = 16.0 * R * R
+    with pytest.raises(ValueError, match="physical limit"):
+        bench.physical_check("forced 8192^2", b, 0.2624e-6, b)
+    # 200 us for the same pivot: 5.4 TB/s, below 8 TB/s
+    assert bench.physical_check("forced 8192^2", b, 200.6e-6, b) == pytest.approx(b / 200.6e-6 / 1e9)
+    # a 16384^2 sweep: HBM-bound working set, limit 8 TB/s (0.5 ms for 4.3 GB would be 8.6 TB/s)
+    b16 = 16.0 * 16384 * 16384
+    with pytest.raises(ValueError):
+        bench.physical_check("sweep", b16, 0.5e-3, 8.0 * 16384 * 16384)
+    assert bench.physical_check("sweep", b16, 0.84e-3, 8.0 * 16384 * 16384) < 8000.0
+    # a cache-resident 1024^2 update (16.8 MB): bounded by the L2 rate, not HBM -- 4.7 us is
+    # legal (3.6 TB/s), the 0.36 us "record" is not (47 TB/s)
+    b1 = 16.0 * 1024 * 1024
+    assert bench.physical_limit_gbs(b1) == bench.L2_AGG_GBS
+    bench.physical_check("forced 1024^2", b1, 4.7e-6, b1)
+    with pytest.raises(ValueError):
+        bench.physical_check("forced 1024^2", b1, 0.3576e-6, b1)
+    with pytest.raises(ValueError):
+        bench.physical_check("zero", b1, 0.0, b1)
+
+
+def test_committed_config_records_are_physical():
+    """Every forced-update / chain record committed from round 4 on passes the guard."""
+    import glob
+    bench = _bench_module()
+    paths = sorted(glob.glob(os.path.join(PROF, "r04*", "configs_2_3*.jsonl")))
+    assert paths, "no round-4 configs record"
+    for p in paths:
+        with open(p) as fh:
+            for ln in fh:
+                if not ln.startswith("{"):
+                    continue
+                rec = json.loads(ln)
+                if "forced_update_us" in rec:
+                    b = 16.0 * rec["size"] ** 2
+                    bench.physical_check(p, b, rec["forced_update_us"] * 1e-6, b)
+
+
+def test_forced_record_agrees_with_rocprof():
+    """The 8192^2 forced-update line (HIP events around the graph replay on the solver stream)
+    agrees with the rocprofv3 kernel trace of the same tool run (k_update<kForced = 2, ...>)."""
+    with open(os.path.join(PROF, "r04a", "configs_2_3.jsonl")) as fh:
+        rec = [json.loads(ln) for ln in fh if '"forced_update_us"' in ln and '"size": 8192' in ln][0]
+    prof_us = _rocprof_avg_ms("r04a/kernel_stats_run_configs3.csv", "k_update<2,") * 1e3
+    assert abs(rec["forced_update_us"] - prof_us) / prof_us < 0.05, (rec, prof_us)
