@@ -95,6 +95,9 @@ def parse():
                     help="row-sharded block path: exchange per pivot (full = all-gather of every "
                          "rank's header + 2 candidate rows; light = header all-gather + one "
                          "max all-reduce of the pivot row; auto = light from 4 ranks on)")
+    ap.add_argument("--enqueue-probe", action="store_true",
+                    help="row-sharded block path: after the timed region, time the host enqueue "
+                         "per pivot of the eager and graph-captured chains (host_enqueue)")
     return ap.parse_args()
 
 

@@ -333,7 +333,12 @@ int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t coun
  * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
  * entries) and the chain's total. */
 int smx_tune_block(int32_t pivots);
-/* Pipelined block chains (default 1): with more than one block, block b+1 is planned on a second
+/* Layout of the block sweep (k_blk_sweep, csrc/smx_block.hpp): 0 automatic (the default: pivot-
+ * row slices in registers up to 12 pivots per sweep, in LDS shared by a workgroup's waves beyond,
+ * and wherever the register layout's grid cannot give every wave one column chunk), 4 registers,
+ * 5 LDS; any other value keeps the setting.  Returns the previous one.  Same bits either way. */
+int smx_tune_block_form(int32_t form);
+/* Pipelined block chains (default 0): with more than one block, block b+1 is planned on a second
  * stream of the library while block b is swept (from block b's input table, every chain prefixed
  * by block b's pivots), the sweeps work out of place, the ragged block comes first, and a final
  * settle kernel restores the buf[(parity + d) & 1] convention when a terminal outcome cut the

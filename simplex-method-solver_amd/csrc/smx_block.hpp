@@ -56,7 +56,7 @@ struct SmxBool {
 // planner leaves the critical path: a block costs one sweep instead of one sweep + P planner
 // launches.  Where the final table lands then depends on the blocks actually swept; a last
 // k_blk_settle moves it to buf[(parity + d) & 1] when a terminal outcome cut the chain.
-constexpr int kBlkMax = 16;          // pivots per block (mul row stride)
+constexpr int kBlkMax = 24;          // pivots per block (mul row stride)
 constexpr int kBlkSlots = kBlkMax + 2;   // record / cf slots: steps 1..P-1, and two for step 0
 // Planner workgroups: four waves, one per select partial.  (Tried: one-wave workgroups, four per
 // partial -- the same threads over 256 CUs instead of 64; every workgroup then merges 256 records
@@ -162,7 +162,7 @@ __device__ __forceinline__ uint32_t win_term(double n) {
     return t;
 }
 
-// Bounded operands: the sweep's unchecked fast path (blk_sweep_body_row1).  A unit needs no
+// Bounded operands: the sweep's unchecked fast path (blk_sweep_body_flag).  A unit needs no
 // per-element window tracking when every pivot element e_q, every pivot-row value p_q[j] of the
 // wave's chunk and every multiplier mq_q of the row lies in [2^-100, 2^101) in magnitude (bnd_term
 // < kBndSpan; zeros, denormals, infinities and NaN fall outside) and the unit's input elements are
@@ -803,6 +803,9 @@ __device__ __forceinline__ bool blk_step_body(
     __syncthreads();
     SMX_BLK_STAMP(1);
     if (stopped) {
+        // Everything decoded above (s_d, s_nb, s_c, s_off from the records or the gathered
+        // headers) is stale on a stopped chain: nothing derived from it may be dereferenced
+        // before this return (test_gpu_block_sharded: a terminal block followed by more blocks).
         if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
         return true;
     }
@@ -1258,41 +1261,20 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step_lag(SMX_BLK_STEP_PARAMS) {
 #undef SMX_BLK_STEP_ARGS
 
 // The sweep: T_k -> T_{k+P} for every element (P = peff pivots of this block).
-// Exact per element with either division (fd_div's window form is bit-identical inside its
-// window; smx_resident.hpp).  Fast path for a unit whose row is not a pivot row and whose chunk
-// holds no pivot column: numerators in the window form, with the smallest and largest |num| of
-// the whole chain tracked per lane; ONE wave vote per unit checks them against the window (and
-// the result against NaN) and otherwise the unit is recomputed with the hardware division.
-template <int P>
-__device__ __forceinline__ dbl2 blk_exact(dbl2 v, int row, int j, const int* rq, const int* cq,
-                                          const double* eq, const dbl2* prs, const double* pc) {
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            const int jj = j + hh;
-            double num;
-            if (row == rq[q]) {
-                num = (jj == cq[q]) ? 1.0 : -v[hh];
-            } else {
-                const double a = v[hh] * eq[q];
-                const double b = prs[q][hh] * pc[q];
-                num = (jj == cq[q]) ? v[hh] : (a - b);
-            }
-            v[hh] = num / eq[q];
-        }
-    }
-    return v;
-}
+// Every element runs the P steps of chain() (above); the division takes the hoisted-reciprocal
+// form where the operands allow it (the domains below) and the IEEE division otherwise.
 
-// blk_exact with the pivots' rows and columns read from the header as it goes (the flag form's
-// rare path: no registers held for them across the sweep)
-template <int P>
+// The exact path of one unit (two adjacent columns of one row): every rule of simplex.py:155-175
+// with the hardware division, the pivots' rows and columns read from the header as it goes (the
+// rare path: no registers held for them across the sweep).  prs(q) returns the chunk's pivot-row
+// values of pivot q at this lane's two columns.
+template <int P, class PRS>
 __device__ __forceinline__ dbl2 blk_exact_h(dbl2 v, int row, int j, const BlkHdr* __restrict__ h,
-                                            const double* eq, const dbl2* prs, const double* pc) {
+                                            const double* eq, PRS prs, const double* pc) {
 #pragma unroll
     for (int q = 0; q < P; ++q) {
         const int rq = h->r[q], cq = h->c[q];
+        const dbl2 p = prs(q);
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
             const int jj = j + hh;
@@ -1301,7 +1283,7 @@ __device__ __forceinline__ dbl2 blk_exact_h(dbl2 v, int row, int j, const BlkHdr
                 num = (jj == cq) ? 1.0 : -v[hh];
             } else {
                 const double a = v[hh] * eq[q];
-                const double b = prs[q][hh] * pc[q];
+                const double b = p[hh] * pc[q];
                 num = (jj == cq) ? v[hh] : (a - b);
             }
             v[hh] = num / eq[q];
@@ -1310,609 +1292,118 @@ __device__ __forceinline__ dbl2 blk_exact_h(dbl2 v, int row, int j, const BlkHdr
     return v;
 }
 
-template <int P, bool NTL>
-__device__ __forceinline__ void blk_sweep_body(const double* Tin, double* Tout, int64_t ld, int R,
-                                               int C, const BlkHdr* __restrict__ h,
-                                               const double* __restrict__ pr,
-                                               const double* __restrict__ mul) {
-    const int lane = threadIdx.x & (kWave - 1);
-    int rq[P], cq[P];
-    double eq[P], yq[P];
-    bool allok = true;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        rq[q] = h->r[q];
-        cq[q] = h->c[q];
-        eq[q] = h->e[q];
-        yq[q] = h->y[q];
-        allok = allok && h->ok[q] != 0;
-    }
-    constexpr int kChunk = 2 * kWave;
-    constexpr int U = 2;
-    const int NW = (int)gridDim.x * kUpdWaves;
-    const int w = (int)blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nchunks = (C + kChunk - 1) / kChunk;
-    const int64_t units = (int64_t)nchunks * R;
-    const int qs = NW / nchunks, rs = NW % nchunks;
-    int i = w / nchunks, ch = w % nchunks;
-    int ch_pr = -1;
-    uint32_t cbits = 0;   // bit 2q+hh: column j+hh of this chunk is pivot q's column
-    dbl2 prs[P];
-    for (int64_t u = w; u < units; u += (int64_t)U * NW) {
-        int ii[U], cc[U];
-        dbl2 x[U];
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            ii[k] = i;
-            cc[k] = ch;
-            ch += rs;
-            i += qs;
-            if (ch >= nchunks) {
-                ch -= nchunks;
-                ++i;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const int j = cc[k] * kChunk + 2 * lane;
-            x[k] = dbl2{0.0, 0.0};
-            if (ii[k] < R && j < C) x[k] = ld2<NTL>(Tin + (int64_t)ii[k] * ld + j);
-        }
-#pragma unroll
-        for (int k = 0; k < U; ++k) {
-            const int row = ii[k];
-            if (row >= R) continue;
-            const int j = cc[k] * kChunk + 2 * lane;
-            if (cc[k] != ch_pr) {
-                ch_pr = cc[k];
-                cbits = 0;
-#pragma unroll
-                for (int q = 0; q < P; ++q) {
-                    prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
-                                     : dbl2{0.0, 0.0};
-                    cbits |= (cq[q] == j ? 1u : 0u) << (2 * q);
-                    cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
-                }
-            }
-            const double* mr = mul + (int64_t)row * kBlkMax;
-            double pc[P];
-            bool special = !allok;
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                pc[q] = mr[q];
-                special = special || row == rq[q];
-            }
-            dbl2 v = x[k];
-            if (!special) {
-                uint32_t wt = 0;
-#pragma unroll
-                for (int q = 0; q < P; ++q) {
-#pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        const double a = v[hh] * eq[q];
-                        const double b = prs[q][hh] * pc[q];
-                        // the pivot column's numerator is the element itself (simplex.py:159-160)
-                        const double num = ((cbits >> (2 * q + hh)) & 1u) ? v[hh] : a - b;
-                        wt = max(wt, win_term(num));
-                        const double t = num * yq[q];          // fd_div inside its window
-                        const double rr = fma(-eq[q], t, num);
-                        v[hh] = fma(rr, yq[q], t);
-                    }
-                }
-                if (!__all(wt < kWinSpan)) v = blk_exact<P>(x[k], row, j, rq, cq, eq, prs, pc);
-            } else {
-                v = blk_exact<P>(v, row, j, rq, cq, eq, prs, pc);
-            }
-            if (j < C)
-                __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(Tout + (int64_t)row * ld + j));
-        }
-    }
-}
-
-// The sweep when every wave keeps one chunk for the whole pass (the grid's wave count is a
-// multiple of the chunks per row, update_grid's usual shape): the pivot-row slices are loaded
-// once, and the two units of a batch are computed together -- one "neither is special" branch,
-// their four element chains interleaved (ILP 4 instead of 2; tools/glds_probe.hip k_reg2:
-// 1120-1184 us vs 1176-1293 us at P = 8), one vote for both.  Same values as blk_sweep_body.
-// Batch index (rows base + t*qs, batch t >> 1) of pivot q's row on this wave, lane q of the
-// wave holding it (0x7fffffff: another wave's row, or no pivot q)
-template <int P, int ROWS = 2>
-__device__ __forceinline__ int blk_special_batch(const BlkHdr* __restrict__ h, int base, int qs) {
-    const int q = threadIdx.x & (kWave - 1);
-    int tb = 0x7fffffff;
-    if (q < P) {
-        const int rq = h->r[q];
-        const int d = rq - base;
-        if (rq >= 0 && d >= 0 && d % qs == 0) tb = (d / qs) / ROWS;
-    }
-    return tb;
-}
-
-// smallest batch index > t among lanes 0..P-1 of tb (wave-uniform)
-template <int P>
-__device__ __forceinline__ int blk_next_batch(int tb, int t) {
-    int best = 0x7fffffff;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        const int v = __builtin_amdgcn_readlane(tb, q);
-        best = (v > t && v < best) ? v : best;
-    }
-    return best;
-}
-
-template <int P, bool NTL, bool PF, int DEPTH = 1>
-__device__ __forceinline__ void blk_sweep_body_fixed(const double* Tin, double* Tout, int64_t ld,
-                                                     int R, int C, const BlkHdr* __restrict__ h,
-                                                     const double* __restrict__ pr,
-                                                     const double* __restrict__ mul) {
-    const int lane = threadIdx.x & (kWave - 1);
-    int rq[P], cq[P];
-    double eq[P], yq[P];
-    bool allok = true;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        rq[q] = h->r[q];
-        cq[q] = h->c[q];
-        eq[q] = h->e[q];
-        yq[q] = h->y[q];
-        allok = allok && h->ok[q] != 0;
-    }
-    constexpr int kChunk = 2 * kWave;
-    const int NW = (int)gridDim.x * kUpdWaves;
-    const int w = (int)blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nchunks = (C + kChunk - 1) / kChunk;
-    const int qs = NW / nchunks;
-    const int ch = w % nchunks;
-    const int j = ch * kChunk + 2 * lane;
-    const int c0 = ch * kChunk;
-    dbl2 prs[P];
-    // a chunk holding a pivot column takes the fast path with the column's numerator selected
-    // (the element itself, simplex.py:159-160) instead of the exact path for all its rows: those
-    // waves were the sweep's stragglers (1.10-1.16 ms -> 0.83-0.90 ms per 8-pivot sweep at
-    // 16384^2, tools/sweep_probe.hip)
-    bool colchunk = false;
-    uint32_t cbits = 0;   // bit 2q+hh: column j+hh is pivot q's column
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
-                         : dbl2{0.0, 0.0};
-        colchunk = colchunk || (cq[q] >= c0 && cq[q] < c0 + kChunk);
-        cbits |= (cq[q] == j ? 1u : 0u) << (2 * q);
-        cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
-    }
-    const bool cspecial = !allok;
-    // the unchecked fast path for this wave's chunk (kBndSpan; as blk_sweep_body_row1)
-    uint32_t pt = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        pt = max(pt, bnd_term(eq[q]));
-        if (j < C) pt = max(pt, bnd_term(prs[q][0]));
-        if (j + 1 < C) pt = max(pt, bnd_term(prs[q][1]));
-    }
-    const bool chunk_free = g_blk_nofree == 0 && !colchunk && __all(pt < kBndSpan);
-    const int base = w / nchunks;
-    const int tbq = blk_special_batch<P>(h, base, qs);
-    int tsp = blk_next_batch<P>(tbq, -1);
-    // one batch: rows i0 and i1 = i0 + qs (batch t), their loads x0 / x1 already issued
-    auto batch = [&](dbl2 x0, dbl2 x1, int i0, int t) {
-        const int i1 = i0 + qs;
-        const bool h1 = i1 < R;
-        const double* m0 = mul + (int64_t)i0 * kBlkMax;
-        const double* m1 = mul + (int64_t)(h1 ? i1 : i0) * kBlkMax;
-        double pc0[P], pc1[P];
-        const bool special = cspecial || !h1 || t == tsp;
-        if (t == tsp) tsp = blk_next_batch<P>(tbq, t);
-        uint32_t mt = 0;   // the two rows' multipliers (uniform: scalar ops)
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            pc0[q] = m0[q];
-            pc1[q] = m1[q];
-            mt = max(mt, max(bnd_term(pc0[q]), bnd_term(pc1[q])));
-        }
-        dbl2 v0 = x0, v1 = x1;
-        bool ok = false;
-        auto fast_free = [&]() {
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const double e = eq[q], y = yq[q];
-                double n[4];
-                n[0] = v0[0] * e - prs[q][0] * pc0[q];
-                n[1] = v0[1] * e - prs[q][1] * pc0[q];
-                n[2] = v1[0] * e - prs[q][0] * pc1[q];
-                n[3] = v1[1] * e - prs[q][1] * pc1[q];
-                double rr[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const double tq = n[k] * y;
-                    const double r = fma(-e, tq, n[k]);
-                    rr[k] = fma(r, y, tq);
-                }
-                v0 = dbl2{rr[0], rr[1]};
-                v1 = dbl2{rr[2], rr[3]};
-            }
-            ok = true;
-        };
-        // the fast path: numerators in the window form, one integer window term per element
-        auto fast = [&](auto selc) {
-            constexpr bool SEL = decltype(selc)::value;
-            uint32_t wt = 0;
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const double e = eq[q], y = yq[q];
-                double n[4];
-                n[0] = v0[0] * e - prs[q][0] * pc0[q];
-                n[1] = v0[1] * e - prs[q][1] * pc0[q];
-                n[2] = v1[0] * e - prs[q][0] * pc1[q];
-                n[3] = v1[1] * e - prs[q][1] * pc1[q];
-                if (SEL) {
-                    const bool s0 = (cbits >> (2 * q)) & 1u, s1 = (cbits >> (2 * q + 1)) & 1u;
-                    n[0] = s0 ? v0[0] : n[0];
-                    n[1] = s1 ? v0[1] : n[1];
-                    n[2] = s0 ? v1[0] : n[2];
-                    n[3] = s1 ? v1[1] : n[3];
-                }
-                double rr[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    wt = max(wt, win_term(n[k]));
-                    const double tq = n[k] * y;               // fd_div inside its window
-                    const double r = fma(-e, tq, n[k]);
-                    rr[k] = fma(r, y, tq);
-                }
-                v0 = dbl2{rr[0], rr[1]};
-                v1 = dbl2{rr[2], rr[3]};
-            }
-            ok = __all(wt < kWinSpan);   // NaN / inf / zero numerators fall outside the window
-        };
-        if (!special) {
-            const uint32_t xt = max(max((uint32_t)__double2hiint(x0[0]) << 1,
-                                        (uint32_t)__double2hiint(x0[1]) << 1),
-                                    max((uint32_t)__double2hiint(x1[0]) << 1,
-                                        (uint32_t)__double2hiint(x1[1]) << 1));
-            if (chunk_free && mt < kBndSpan && __all(xt < kBndXMax))
-                fast_free();
-            else if (colchunk)
-                fast(SmxBool<true>{});
-            else
-                fast(SmxBool<false>{});
-        }
-        if (!ok) {
-            if (PF) {
-                // reloaded (this batch's elements are not written yet, even in place), so the
-                // inputs need not stay live beside the chains
-                const int jl = min(j, (C - 1) & ~1);
-                x0 = *reinterpret_cast<const dbl2*>(Tin + (int64_t)i0 * ld + jl);
-                if (h1) x1 = *reinterpret_cast<const dbl2*>(Tin + (int64_t)i1 * ld + jl);
-            }
-            v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
-            if (h1) v1 = blk_exact<P>(x1, i1, j, rq, cq, eq, prs, pc1);
-        }
-        if (j < C) {
-            __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
-            if (h1)
-                __builtin_nontemporal_store(v1,
-                                            reinterpret_cast<dbl2*>(Tout + (int64_t)i1 * ld + j));
-        }
-    };
-    if (!PF) {
-        int t = 0;
-        for (int i0 = base; i0 < R; i0 += 2 * qs, ++t) {
-            const int i1 = i0 + qs;
-            dbl2 x0 = dbl2{0.0, 0.0}, x1 = dbl2{0.0, 0.0};
-            if (j < C) {
-                x0 = ld2<NTL>(Tin + (int64_t)i0 * ld + j);
-                if (i1 < R) x1 = ld2<NTL>(Tin + (int64_t)i1 * ld + j);
-            }
-            batch(x0, x1, i0, t);
-        }
-        return;
-    }
-    // PF: the loads of the next DEPTH batches are issued before this batch's arithmetic, into a
-    // ring of DEPTH + 1 register sets, without branches (row and column clamped into the table; a
-    // clamped row's or lane's values are never stored).  The loads are inline asm with explicit
-    // waits: the compiler's own vmcnt tracking waits for them at the loop edge.  In-order vmcnt
-    // (gfx9 counts loads and stores): before a set is used, the ops issued after its loads are
-    // the other DEPTH sets' loads (two each) and one batch's two stores per set consumed since
-    // (every wave holds a lane j < C, and only the last batch, after which nothing waits, lacks
-    // row i1) -- 4 * DEPTH in the steady state, fewer for the first sets (the exact count is
-    // waited for: a larger one would let a set be used before its loads land).
-    const int jc = min(j, (C - 1) & ~1);
-    auto ldc = [&](int row) {
-        dbl2 v;
-        const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
-        if (NTL)
-            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
-        else
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-        return v;
-    };
-    if constexpr (DEPTH == 1) {
-        dbl2 a0 = ldc(base), a1 = ldc(base + qs);
-        dbl2 b0 = ldc(base + 2 * qs), b1 = ldc(base + 3 * qs);
-        asm volatile("s_waitcnt vmcnt(2)" : "+v"(a0), "+v"(a1) :: "memory");
-        int t = 0;
-        for (int i0 = base; i0 < R; i0 += 4 * qs, t += 2) {
-            batch(a0, a1, i0, t);
-            if (i0 + 2 * qs >= R) break;
-            a0 = ldc(i0 + 4 * qs);
-            a1 = ldc(i0 + 5 * qs);
-            asm volatile("s_waitcnt vmcnt(4)" : "+v"(b0), "+v"(b1) :: "memory");
-            batch(b0, b1, i0 + 2 * qs, t + 1);
-            if (i0 + 4 * qs >= R) break;
-            b0 = ldc(i0 + 6 * qs);
-            b1 = ldc(i0 + 7 * qs);
-            asm volatile("s_waitcnt vmcnt(4)" : "+v"(a0), "+v"(a1) :: "memory");
-        }
-    } else {
-        static_assert(DEPTH == 2, "prefetch depth 1 or 2");
-        dbl2 a0 = ldc(base), a1 = ldc(base + qs);
-        dbl2 b0 = ldc(base + 2 * qs), b1 = ldc(base + 3 * qs);
-        dbl2 c0 = ldc(base + 4 * qs), c1 = ldc(base + 5 * qs);
-        asm volatile("s_waitcnt vmcnt(4)" : "+v"(a0), "+v"(a1) :: "memory");
-        int t = 0;
-        for (int i0 = base; i0 < R; i0 += 6 * qs, t += 3) {
-            batch(a0, a1, i0, t);
-            if (i0 + 2 * qs >= R) break;
-            a0 = ldc(i0 + 6 * qs);
-            a1 = ldc(i0 + 7 * qs);
-            if (t == 0)   // after b's first loads: c's loads, a's stores, a's next loads
-                asm volatile("s_waitcnt vmcnt(6)" : "+v"(b0), "+v"(b1) :: "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(8)" : "+v"(b0), "+v"(b1) :: "memory");
-            batch(b0, b1, i0 + 2 * qs, t + 1);
-            if (i0 + 4 * qs >= R) break;
-            b0 = ldc(i0 + 8 * qs);
-            b1 = ldc(i0 + 9 * qs);
-            asm volatile("s_waitcnt vmcnt(8)" : "+v"(c0), "+v"(c1) :: "memory");
-            batch(c0, c1, i0 + 4 * qs, t + 2);
-            if (i0 + 6 * qs >= R) break;
-            c0 = ldc(i0 + 10 * qs);
-            c1 = ldc(i0 + 11 * qs);
-            asm volatile("s_waitcnt vmcnt(8)" : "+v"(a0), "+v"(a1) :: "memory");
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no load in flight at exit
-}
-
-// The fixed-chunk sweep with ONE row per batch (two element chains per lane): half the per-row
-// multipliers live at a time (P instead of 2 P scalar registers), so large P does not spill
-// scalars into vector lanes inside the loop.  Next row's load issued before this row's
-// arithmetic (prefetch depth 1).  Same values as blk_sweep_body.
-template <int P, bool NTL>
-__device__ __forceinline__ void blk_sweep_body_row1(const double* Tin, double* Tout, int64_t ld,
-                                                    int R, int C, const BlkHdr* __restrict__ h,
-                                                    const double* __restrict__ pr,
-                                                    const double* __restrict__ mul) {
-    const int lane = threadIdx.x & (kWave - 1);
-    int rq[P], cq[P];
-    double eq[P], yq[P];
-    bool allok = true;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        rq[q] = h->r[q];
-        cq[q] = h->c[q];
-        eq[q] = h->e[q];
-        yq[q] = h->y[q];
-        allok = allok && h->ok[q] != 0;
-    }
-    constexpr int kChunk = 2 * kWave;
-    const int NW = (int)gridDim.x * kUpdWaves;
-    const int w = (int)blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int nchunks = (C + kChunk - 1) / kChunk;
-    const int qs = NW / nchunks;
-    const int ch = w % nchunks;
-    const int j = ch * kChunk + 2 * lane;
-    const int c0 = ch * kChunk;
-    dbl2 prs[P];
-    bool colchunk = false;
-    uint32_t cbits = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
-                         : dbl2{0.0, 0.0};
-        colchunk = colchunk || (cq[q] >= c0 && cq[q] < c0 + kChunk);
-        cbits |= (cq[q] == j ? 1u : 0u) << (2 * q);
-        cbits |= (cq[q] == j + 1 ? 1u : 0u) << (2 * q + 1);
-    }
-    const bool cspecial = !allok;
-    // the unchecked fast path (kBndSpan) for this wave's chunk: bounded pivot elements and
-    // pivot-row values, no pivot column in the chunk (g_blk_nofree: A/B experiments only)
-    const bool kNoFree = g_blk_nofree != 0;
-    uint32_t pt = 0;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        pt = max(pt, bnd_term(eq[q]));
-        if (j < C) pt = max(pt, bnd_term(prs[q][0]));
-        if (j + 1 < C) pt = max(pt, bnd_term(prs[q][1]));
-    }
-    const bool chunk_free = !kNoFree && !colchunk && __all(pt < kBndSpan);
-    const int base = w / nchunks;
-    const int tbq = blk_special_batch<P, 1>(h, base, qs);
-    int tsp = blk_next_batch<P>(tbq, -1);
-    auto row1 = [&](dbl2 x0, int i0, int t) {
-        const double* m0 = mul + (int64_t)i0 * kBlkMax;
-        double pc0[P];
-        const bool special = cspecial || t == tsp;
-        if (t == tsp) tsp = blk_next_batch<P>(tbq, t);
-        uint32_t mt = 0;   // the row's multipliers (uniform: scalar ops)
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            pc0[q] = m0[q];
-            mt = max(mt, bnd_term(pc0[q]));
-        }
-        dbl2 v0 = x0;
-        bool ok = false;
-        auto fast_free = [&]() {
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const double e = eq[q], y = yq[q];
-                double n[2];
-                n[0] = v0[0] * e - prs[q][0] * pc0[q];
-                n[1] = v0[1] * e - prs[q][1] * pc0[q];
-                double rr[2];
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const double tq = n[k] * y;
-                    const double r = fma(-e, tq, n[k]);
-                    rr[k] = fma(r, y, tq);
-                }
-                v0 = dbl2{rr[0], rr[1]};
-            }
-            ok = true;
-        };
-        auto fast = [&](auto selc) {
-            constexpr bool SEL = decltype(selc)::value;
-            uint32_t wt = 0;
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const double e = eq[q], y = yq[q];
-                double n[2];
-                n[0] = v0[0] * e - prs[q][0] * pc0[q];
-                n[1] = v0[1] * e - prs[q][1] * pc0[q];
-                if (SEL) {
-                    const bool s0 = (cbits >> (2 * q)) & 1u, s1 = (cbits >> (2 * q + 1)) & 1u;
-                    n[0] = s0 ? v0[0] : n[0];
-                    n[1] = s1 ? v0[1] : n[1];
-                }
-                double rr[2];
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    wt = max(wt, win_term(n[k]));
-                    const double tq = n[k] * y;
-                    const double r = fma(-e, tq, n[k]);
-                    rr[k] = fma(r, y, tq);
-                }
-                v0 = dbl2{rr[0], rr[1]};
-            }
-            ok = __all(wt < kWinSpan);
-        };
-        if (!special) {
-            const uint32_t xt = max((uint32_t)__double2hiint(x0[0]) << 1,
-                                    (uint32_t)__double2hiint(x0[1]) << 1);
-            if (chunk_free && mt < kBndSpan && __all(xt < kBndXMax))
-                fast_free();
-            else if (colchunk)
-                fast(SmxBool<true>{});
-            else
-                fast(SmxBool<false>{});
-        }
-        if (!ok) {
-            const int jl = min(j, (C - 1) & ~1);
-            x0 = *reinterpret_cast<const dbl2*>(Tin + (int64_t)i0 * ld + jl);
-            v0 = blk_exact<P>(x0, i0, j, rq, cq, eq, prs, pc0);
-        }
-        if (j < C)
-            __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
-    };
-    // prefetch depth 1 over single rows: before a register set is used, the ops issued after
-    // its load are the previous row's store and the other set's load (vmcnt(2); vmcnt(1) first)
-    const int jc = min(j, (C - 1) & ~1);
-    auto ldc = [&](int row) {
-        dbl2 v;
-        const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
-        if (NTL)
-            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
-        else
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-        return v;
-    };
-    dbl2 a = ldc(base), b = ldc(base + qs);
-    asm volatile("s_waitcnt vmcnt(1)" : "+v"(a) :: "memory");
-    int t = 0;
-    for (int i0 = base; i0 < R; i0 += 2 * qs, t += 2) {
-        row1(a, i0, t);
-        if (i0 + qs >= R) break;
-        a = ldc(i0 + 2 * qs);
-        asm volatile("s_waitcnt vmcnt(2)" : "+v"(b) :: "memory");
-        row1(b, i0 + qs, t + 1);
-        if (i0 + 2 * qs >= R) break;
-        b = ldc(i0 + 3 * qs);
-        asm volatile("s_waitcnt vmcnt(2)" : "+v"(a) :: "memory");
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// The one-row sweep with the planner's per-row flags (blk_rflags): the unchecked fast path needs a
-// bounded chunk (e and the chunk's pivot-row values in [2^-100, 2^101), checked once per sweep), a
-// flagged row (no pivot row, every multiplier bounded: the planner checked them when it computed
-// them) and bounded inputs (one vote per row).  Re-checking the row's P multipliers in the sweep
-// cost ~30 scalar and ~12 vector instructions per row beside the 120 fp64 ones, and the row's
-// branch waited on them: tools/sweep_lab.hip, 16384^2, P = 10: 894 -> 753 us per sweep
-// (profiles/r03/sweep_lab.jsonl).  The fast path is straight-line: a per-pivot (uniform, never
-// taken) branch to select a pivot column's numerator cost another ~20 % (lab V7 vs V6), so pivot
-// columns are NOT special here.  On a flagged row the pivot column's lane computes
-// RN(x e) - RN(e x) = +0 at its step (its element IS mul[i][q] there) and carries harmless finite
-// values after it; blk_fixcols (k_blk_sweep_rest) then rewrites every pivot column from the planner's multipliers.
-// Rows or chunks outside the fast domain take the window-tracked path (a pivot column's zero
-// numerator fails its vote), then the exact path, which applies every rule itself.
-// SMX_FLAG_FASTONLY: diagnostic build only (tools/sweep_prod_probe.hip): the fast path, then the
-// exact one -- no zero-safe or window-tracked path in the loop
-#ifdef SMX_FLAG_FASTONLY
-constexpr bool kDiagFastOnly = true;
-#else
-constexpr bool kDiagFastOnly = false;
-#endif
-template <int P, bool NTL>
+// The flag-form sweep: one row per step of a wave, the planner's per-row flags (blk_rflags) instead
+// of per-row checks.  The unchecked fast path needs a bounded chunk (e and the chunk's pivot-row
+// values in [2^-100, 2^101), checked once per sweep), a flagged row (no pivot row, every
+// multiplier bounded: the planner checked them when it computed them) and bounded inputs (one vote
+// per row).  Re-checking the row's P multipliers in the sweep cost ~30 scalar and ~12 vector
+// instructions per row beside the 120 fp64 ones, and the row's branch waited on them:
+// tools/sweep_lab.hip, 16384^2, P = 10: 894 -> 753 us per sweep (profiles/r03/sweep_lab.jsonl).
+// The fast path is straight-line: a per-pivot (uniform, never taken) branch to select a pivot
+// column's numerator cost another ~20 % (lab V7 vs V6), so pivot columns are NOT special here.  On
+// a flagged row the pivot column's lane computes RN(x e) - RN(e x) = +0 at its step (its element
+// IS mul[i][q] there) and carries harmless finite values after it; blk_fixcols (k_blk_sweep_rest)
+// then rewrites every pivot column from the planner's multipliers.  Rows or chunks outside the fast
+// domain take the window-tracked path (a pivot column's zero numerator fails its vote), then the
+// exact path, which applies every rule itself.
+//
+// Two layouts (FORM):
+//  4  wave-chunk: every wave keeps one 128-column chunk (w % nchunks) for the whole pass, its
+//     pivot-row slices in registers (2P doubles per lane) and e / y in scalar registers -- the
+//     fastest up to ~12 pivots (profiles/r03/, tools/sweep_lab2.hip V1);
+//  5  workgroup-chunk: the four waves of a workgroup share one chunk (blockIdx % nchunks) and its
+//     pivot-row slices live in LDS (P KiB per workgroup), (e, y) pairs in LDS as well: ~60-70
+//     VGPRs at any P, so 16-24 pivots per sweep keep 7-8 waves per SIMD instead of spilling
+//     scalars (tools/sweep_lab2.hip V3 / V6, profiles/r04b/lab2.jsonl: P = 20 1.33 ms vs 1.43 ms
+//     for the register layout at 16384^2).
+template <int P, int FORM>
 __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* Tout, int64_t ld,
                                                     int R, int C, const BlkHdr* __restrict__ h,
                                                     const double* __restrict__ pr,
                                                     const double* __restrict__ mul) {
+    constexpr bool LDS = FORM == 5;
+    __shared__ dbl2 s_pr[LDS ? P : 1][kWave];
+    __shared__ dbl2 s_ey[LDS ? P : 1];
     const int32_t* __restrict__ rfl = blk_rflags(mul, R);
     const int lane = threadIdx.x & (kWave - 1);
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // the pivots' rows and columns are NOT held here: the row flags say which rows are pivot
     // rows, and only the exact path (blk_exact_h) needs the indices, which it reads from h --
     // 2P fewer scalar registers (and spills) in the loop
-    double eq[P], yq[P];
+    double eq[LDS ? 1 : P], yq[LDS ? 1 : P];
     bool allok = true;
 #pragma unroll
-    for (int q = 0; q < P; ++q) {
-        eq[q] = h->e[q];
-        yq[q] = h->y[q];
-        allok = allok && h->ok[q] != 0;
-    }
+    for (int q = 0; q < P; ++q) allok = allok && h->ok[q] != 0;
     constexpr int kChunk = 2 * kWave;
-    const int NW = (int)gridDim.x * kUpdWaves;
-    const int w = (int)blockIdx.x * kUpdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nchunks = (C + kChunk - 1) / kChunk;
-    const int qs = NW / nchunks;
-    const int ch = w % nchunks;
+    int ch, base, qs;
+    if constexpr (LDS) {
+        ch = (int)blockIdx.x % nchunks;
+        base = ((int)blockIdx.x / nchunks) * kUpdWaves + wib;
+        qs = ((int)gridDim.x / nchunks) * kUpdWaves;
+    } else {
+        const int NW = (int)gridDim.x * kUpdWaves;
+        const int w = (int)blockIdx.x * kUpdWaves + wib;
+        ch = w % nchunks;
+        base = w / nchunks;
+        qs = NW / nchunks;
+    }
     const int j = ch * kChunk + 2 * lane;
-    dbl2 prs[P];
+    dbl2 prs[LDS ? 1 : P];
+    if constexpr (LDS) {
+        for (int t = threadIdx.x; t < P * kWave; t += kUpdBlock) {
+            const int q = t / kWave, jl = ch * kChunk + 2 * (t % kWave);
+            s_pr[q][t % kWave] = jl < C ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + jl)
+                                        : dbl2{0.0, 0.0};
+        }
+        if (threadIdx.x < P) s_ey[threadIdx.x] = dbl2{h->e[threadIdx.x], h->y[threadIdx.x]};
+        __syncthreads();
+    } else {
 #pragma unroll
-    for (int q = 0; q < P; ++q)
-        prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
-                         : dbl2{0.0, 0.0};
+        for (int q = 0; q < P; ++q) {
+            eq[q] = h->e[q];
+            yq[q] = h->y[q];
+            prs[q] = (j < C) ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + j)
+                             : dbl2{0.0, 0.0};
+        }
+    }
+    auto PR = [&](int q) -> dbl2 {
+        if constexpr (LDS) return s_pr[q][lane];
+        else return prs[q];
+    };
+    auto EY = [&](int q) -> dbl2 {
+        if constexpr (LDS) return s_ey[q];
+        else return dbl2{eq[q], yq[q]};
+    };
     const bool kNoFree = g_blk_nofree != 0;
     uint32_t et = 0, pt = 0;
     bool zok = true;   // every pivot-row value bounded or an exact +-0
 #pragma unroll
     for (int q = 0; q < P; ++q) {
-        et = max(et, bnd_term(eq[q]));
+        const dbl2 p = PR(q);
+        et = max(et, bnd_term(EY(q)[0]));
         if (j < C) {
-            pt = max(pt, bnd_term(prs[q][0]));
-            zok = zok && bnd_or_zero(prs[q][0]);
+            pt = max(pt, bnd_term(p[0]));
+            zok = zok && bnd_or_zero(p[0]);
         }
         if (j + 1 < C) {
-            pt = max(pt, bnd_term(prs[q][1]));
-            zok = zok && bnd_or_zero(prs[q][1]);
+            pt = max(pt, bnd_term(p[1]));
+            zok = zok && bnd_or_zero(p[1]);
         }
     }
     // chunk_free: bounded, no zeros (fast path); chunk_zok: bounded or zero (zero-safe path)
     const bool chunk_zok = !kNoFree && allok && et < kBndSpan && __all(zok);
     const bool chunk_free = chunk_zok && __all(pt < kBndSpan);
-    const int base = w / nchunks;
+    double eqa[P];   // the exact path's pivot elements (loaded there, rare)
     // Every vector load of the loop is this inline asm: a load the compiler can see (the slow
-    // path's reload, as in blk_sweep_body_row1) made it put s_waitcnt vmcnt(0) at the head of the
-    // fast path, waiting for the next row's prefetch before computing this row (sweep 990 us at
-    // P = 10, 16384^2, against 750 us for the lab's loop, tools/sweep_lab.hip).
+    // path's reload) made it put s_waitcnt vmcnt(0) at the head of the fast path, waiting for
+    // the next row's prefetch before computing this row (sweep 990 us at P = 10, 16384^2, against
+    // 750 us for the lab's loop, tools/sweep_lab.hip).
     const int jc = min(j, (C - 1) & ~1);
     auto ldc = [&](int row) {
         dbl2 v;
         const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
-        if (NTL)
-            asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
-        else
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p) : "memory");
         return v;
     };
     auto rowf = [&](dbl2 x0, int i0) {
@@ -1931,79 +1422,106 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         const uint32_t xt = max((uint32_t)__double2hiint(x0[0]) << 1,
                                 (uint32_t)__double2hiint(x0[1]) << 1);
         if (chunk_free && rf == 1 && __all(xt < kBndXMax)) {
-            // the 2P products p * mq first (they do not depend on the chain) and held there:
-            // issued back to back, the chains after them run without waiting on any
-            // (tools/sweep_lab.hip V1: this order, 750-770 us at P = 10, 16384^2; interleaved
-            // with the chains as the compiler otherwise places them, ~850 us)
-            dbl2 bq[P];
+            if constexpr (!LDS) {
+                // the 2P products p * mq first (they do not depend on the chain) and held there:
+                // issued back to back, the chains after them run without waiting on any
+                // (tools/sweep_lab.hip V1: this order, 750-770 us at P = 10, 16384^2; interleaved
+                // with the chains as the compiler otherwise places them, ~850 us)
+                dbl2 bq[P];
 #pragma unroll
-            for (int q = 0; q < P; ++q) bq[q] = dbl2{prs[q][0] * pc0[q], prs[q][1] * pc0[q]};
+                for (int q = 0; q < P; ++q)
+                    bq[q] = dbl2{prs[q][0] * pc0[q], prs[q][1] * pc0[q]};
 #pragma unroll
-            for (int q = 0; q < P; ++q) asm volatile("" : "+v"(bq[q]));
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const double e = eq[q], y = yq[q];
-                double n[2];
-                n[0] = v0[0] * e - bq[q][0];
-                n[1] = v0[1] * e - bq[q][1];
-                double rr[2];
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const double tq = n[k] * y;
-                    const double r = fma(-e, tq, n[k]);
-                    rr[k] = fma(r, y, tq);
-                }
-                v0 = dbl2{rr[0], rr[1]};
-            }
-            ok = true;
-        } else if (!kDiagFastOnly && chunk_zok && (rf & 1) &&
-                   __all(bnd_or_zero(x0[0]) && bnd_or_zero(x0[1]))) {
-            // the zero-extended domain (rf 1 or 3, a chunk or row with exact zeros): the same
-            // arithmetic with fd_zero's v_div_fixup (ONE more instruction per element-pivot)
-            asm volatile("" ::: "memory");   // keeps this path out of the fast path's code
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const double e = eq[q], y = yq[q];
-                double n[2];
-                n[0] = v0[0] * e - prs[q][0] * pc0[q];
-                n[1] = v0[1] * e - prs[q][1] * pc0[q];
-                v0 = dbl2{fd_zero(n[0], e, y), fd_zero(n[1], e, y)};
-            }
-            ok = true;
-        } else if (!kDiagFastOnly) {
-            if (allok && rf != 2) {   // not a pivot row (rf == 2): the window-tracked path
-                // the window-tracked path (numerators checked once per row by a vote)
-                uint32_t wt = 0;
+                for (int q = 0; q < P; ++q) asm volatile("" : "+v"(bq[q]));
 #pragma unroll
                 for (int q = 0; q < P; ++q) {
                     const double e = eq[q], y = yq[q];
                     double n[2];
-                    n[0] = v0[0] * e - prs[q][0] * pc0[q];
-                    n[1] = v0[1] * e - prs[q][1] * pc0[q];
+                    n[0] = v0[0] * e - bq[q][0];
+                    n[1] = v0[1] * e - bq[q][1];
                     double rr[2];
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        wt = max(wt, win_term(n[k]));
                         const double tq = n[k] * y;
                         const double r = fma(-e, tq, n[k]);
                         rr[k] = fma(r, y, tq);
                     }
                     v0 = dbl2{rr[0], rr[1]};
                 }
-                ok = __all(wt < kWinSpan);
+            } else {
+                // products inline: the slices and (e, y) come from LDS per pivot, few registers
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    const dbl2 p = s_pr[q][lane];
+                    const dbl2 ey = s_ey[q];
+                    const double e = ey[0], y = ey[1];
+                    double n[2];
+                    n[0] = v0[0] * e - p[0] * pc0[q];
+                    n[1] = v0[1] * e - p[1] * pc0[q];
+                    double rr[2];
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const double tq = n[k] * y;
+                        const double r = fma(-e, tq, n[k]);
+                        rr[k] = fma(r, y, tq);
+                    }
+                    v0 = dbl2{rr[0], rr[1]};
+                }
             }
+            ok = true;
+        } else if (chunk_zok && (rf & 1) && __all(bnd_or_zero(x0[0]) && bnd_or_zero(x0[1]))) {
+            // the zero-extended domain (rf 1 or 3, a chunk or row with exact zeros): the same
+            // arithmetic with fd_zero's v_div_fixup (ONE more instruction per element-pivot)
+            asm volatile("" ::: "memory");   // keeps this path out of the fast path's code
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const dbl2 p = PR(q);
+                const dbl2 ey = EY(q);
+                const double e = ey[0], y = ey[1];
+                double n[2];
+                n[0] = v0[0] * e - p[0] * pc0[q];
+                n[1] = v0[1] * e - p[1] * pc0[q];
+                v0 = dbl2{fd_zero(n[0], e, y), fd_zero(n[1], e, y)};
+            }
+            ok = true;
+        } else if (allok && rf != 2) {   // not a pivot row (rf == 2): the window-tracked path
+            // numerators checked once per row by a vote
+            uint32_t wt = 0;
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const dbl2 p = PR(q);
+                const dbl2 ey = EY(q);
+                const double e = ey[0], y = ey[1];
+                double n[2];
+                n[0] = v0[0] * e - p[0] * pc0[q];
+                n[1] = v0[1] * e - p[1] * pc0[q];
+                double rr[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    wt = max(wt, win_term(n[k]));
+                    const double tq = n[k] * y;
+                    const double r = fma(-e, tq, n[k]);
+                    rr[k] = fma(r, y, tq);
+                }
+                v0 = dbl2{rr[0], rr[1]};
+            }
+            ok = __all(wt < kWinSpan);
         }
         if (!ok) {
             // reloaded (not written yet, even in place) so x0 need not stay live beside the
             // fast arithmetic; the wait covers the next row's prefetch too (rare path)
             x0 = ldc(i0);
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(x0) :: "memory");
-            v0 = blk_exact_h<P>(x0, i0, j, h, eq, prs, pc0);
+#pragma unroll
+            for (int q = 0; q < P; ++q) eqa[q] = h->e[q];
+            v0 = blk_exact_h<P>(x0, i0, j, h, eqa, PR, pc0);
         }
         if (j < C)
             __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
     };
-    // prefetch depth 1 over single rows (as blk_sweep_body_row1)
+    if (base >= R) return;
+    // prefetch depth 1 over single rows: before a register set is used, the ops issued after
+    // its load are the previous row's store and the other set's load (vmcnt(2); vmcnt(1) first)
     dbl2 a = ldc(base), b = ldc(base + qs);
     asm volatile("s_waitcnt vmcnt(1)" : "+v"(a) :: "memory");
     for (int i0 = base; i0 < R; i0 += 2 * qs) {
@@ -2080,10 +1598,8 @@ __device__ __forceinline__ double* blk_out(double* b_in, double* b_other, int ip
 
 // The sweep of a block that applied all P of its pivots (h->peff == P; otherwise it does nothing
 // and k_blk_sweep_rest handles the block): one body per kernel, so the register allocation is
-// that body's alone.  FORM 0: generic; 1, 2: the launcher made the wave count a multiple of the
-// chunks per row (blk_sweep_body_fixed; at P >= 7 with the next FORM batches' loads issued
-// before this batch's arithmetic).  Output per blk_out.
-template <int P, bool NTL, int FORM>
+// that body's alone.  FORM 4 / 5: blk_sweep_body_flag's layouts.  Output per blk_out.
+template <int P, int FORM>
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b_other, int64_t ld,
                                                          int R, int C,
                                                          const BlkHdr* __restrict__ h,
@@ -2093,14 +1609,7 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
                                                          int in_idx) {
     if (h->peff != P) return;
     double* out = blk_out(b_in, b_other, ipx, in_idx, P, hs);
-    if constexpr (FORM == 4)
-        blk_sweep_body_flag<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
-    else if constexpr (FORM == 3)
-        blk_sweep_body_row1<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
-    else if constexpr (FORM > 0)
-        blk_sweep_body_fixed<P, NTL, (P >= 7), FORM>(b_in, out, ld, R, C, h, pr, mul);
-    else
-        blk_sweep_body<P, NTL>(b_in, out, ld, R, C, h, pr, mul);
+    blk_sweep_body_flag<P, FORM>(b_in, out, ld, R, C, h, pr, mul);
 }
 
 // After k_blk_sweep<P> (one launch, whichever case holds):

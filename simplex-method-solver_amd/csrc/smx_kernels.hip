@@ -455,26 +455,15 @@ using BshPackFn = void (*)(const double*, int64_t, int, int, int, int, int, cons
                            const BlkHdr*, const smx_part*, int, const double*, const double*,
                            double*);
 
-// Kernel tables by pivot count (1..kBlkMax).  Plain (cache-resident) loads are instantiated up to
-// P = 8 only: larger blocks are for tables far beyond the Infinity Cache.
-template <bool NTL, int FORM, int... Is>
+// Sweep kernels by pivot count (1..kBlkMax) and layout (FORM 4 / 5, blk_sweep_body_flag)
+template <int FORM, int... Is>
 BlkSweepFn blk_sweep_pick(int P, std::integer_sequence<int, Is...>) {
-    static const BlkSweepFn t[] = {k_blk_sweep<Is + 1, NTL, FORM>...};
+    static const BlkSweepFn t[] = {k_blk_sweep<Is + 1, FORM>...};
     return t[P - 1];
 }
-
-// form 0 generic, 1 fixed, 2 fixed with two batches prefetched, 3 one row per batch, 4 one row per
-// batch with the planner's row flags (3 and 4: streaming loads only)
-BlkSweepFn blk_sweep_fn(int P, bool ntl, int form) {
+BlkSweepFn blk_sweep_fn(int P, int form) {
     using All = std::make_integer_sequence<int, kBlkMax>;
-    using Low = std::make_integer_sequence<int, 8>;
-    if (ntl || P > 8) {
-        if (form == 4) return blk_sweep_pick<true, 4>(P, All{});
-        if (form == 3) return blk_sweep_pick<true, 3>(P, All{});
-        if (form == 2) return blk_sweep_pick<true, 2>(P, All{});
-        return form ? blk_sweep_pick<true, 1>(P, All{}) : blk_sweep_pick<true, 0>(P, All{});
-    }
-    return form ? blk_sweep_pick<false, 1>(P, Low{}) : blk_sweep_pick<false, 0>(P, Low{});
+    return form == 5 ? blk_sweep_pick<5>(P, All{}) : blk_sweep_pick<4>(P, All{});
 }
 
 template <bool SH, int... Is>
@@ -581,77 +570,53 @@ int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, con
     return (int)hipGetLastError();
 }
 
+// Sweep layout (smx_tune_block_form): 0 automatic -- the register layout (4) up to kSweepRegMaxP
+// pivots, the LDS layout (5) beyond and wherever the register layout's grid cannot give every
+// wave one chunk; 4 / 5 forced (tests, A/B timing).
+int g_block_form = 0;
+constexpr int kSweepRegMaxP = 12;
+
+// Grid of the LDS layout: a multiple of the chunks per row (every workgroup keeps one chunk),
+// as many workgroups as are resident at bpc per CU, at least one per chunk.
+int sweep_grid_lds(const smx_shape& s, int bpc) {
+    const int64_t nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
+    int64_t per = (int64_t)num_cus() * bpc / nchunks;
+    const int64_t rows_per = (s.rows + 1 + kUpdWaves - 1) / kUpdWaves;   // >= 1 row per wave
+    if (per > rows_per) per = rows_per;
+    if (per < 1) per = 1;
+    return (int)(per * nchunks);
+}
+
 // ipx / in_idx: see blk_out (ipx 0: in place when the pivots applied are even, the layout of the
 // unpipelined chains; -1: never in place); plan slot `slot`.
 int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, char* blk,
                        const BlkLayout& L, hipStream_t st, int slot = 0, int ipx = 0,
                        int in_idx = 0, int ipx_part = 0) {
-    const bool ntl = (int64_t)(s.rows + 1) * s.ld * 8 > kCacheTable;
-    // the fixed-chunk form when the grid's wave count is a multiple of the chunks per row, at
-    // the resident block count (occupancy API: P = 8 holds 81 VGPRs -> 5 blocks per CU; asking
-    // for 7 queued 2 of them behind the rest, 932 / 925 vs 918 / 906 us per sweep at 16384^2,
-    // tools/sweep_pmc.py).  SMX_BLK_BPC (experiments): blocks per CU of the fixed form.
-    static const int bpc_env = [] {
-        const char* e = getenv("SMX_BLK_BPC");
-        return e ? atoi(e) : 0;
-    }();
-    // SMX_BLK_DEPTH (experiments): batches prefetched by the fixed form at P >= 7 (1 or 2)
-    static const int depth_env = [] {
-        const char* e = getenv("SMX_BLK_DEPTH");
-        return e ? atoi(e) : 0;
-    }();
-    const int depth = depth_env == 2 ? 2 : 1;
-    // one row per batch from 10 pivots on (blk_sweep_body_row1: fewer scalar spills; 16384^2
-    // sweeps 1054 / 1260 / 1381 us at P = 10 / 12 / 14 vs 1078 / 1282 / 1389 with two rows,
-    // the same at 8: profiles/r02/sweep_rows_ab.jsonl).  SMX_BLK_ROWS (experiments): 1 or 2
-    // rows per batch for every P.
-    static const int rows_env = [] {
-        const char* e = getenv("SMX_BLK_ROWS");
-        return e ? atoi(e) : 0;
-    }();
-    const bool row1 = rows_env == 1 || (rows_env == 0 && P >= 10);
-    // SMX_BLK_FORM (experiments): 1..3 forces an earlier sweep form; default: the flag form (4)
-    static const int form_env = [] {
-        const char* e = getenv("SMX_BLK_FORM");
-        return e ? atoi(e) : 0;
-    }();
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    int form = 4;
-    if (form_env >= 1 && form_env <= 3) form = form_env;
-    if (form == 3 && rows_env == 2) form = P >= 7 ? depth : 1;
-    (void)row1;
-    const bool one_row = form >= 3;
-    BlkSweepFn fn = blk_sweep_fn(P, ntl || one_row, form);
-    // the one-row form at P = 10..12 (72-83 VGPRs): 7 blocks per CU, above the occupancy API's
-    // 6 / 5 -- 1030-1044 vs 1070-1075 us per 10-pivot sweep and 1189-1196 vs 1234-1255 per
-    // 12-pivot sweep at 16384^2 (profiles/r02/sweep_bpc_row1_ab.jsonl; 8 is no better)
-    // the flag form: 5 blocks per CU (all resident at 80 VGPRs), 827-882 vs 855-901 us per
-    // 10-pivot sweep at 16384^2 over 7 (profiles/r03/bpc_ab.jsonl)
-    const int bpc_sweep = bpc_env > 0 ? bpc_env
-                                      : (one_row && P <= 12 ? (form == 4 ? 5 : 7) : 0);
-    int grid = update_grid(s, (const void*)fn, 0, bpc_sweep);
-    if (((int64_t)grid * kUpdWaves) % nchunks != 0) {
-        fn = blk_sweep_fn(P, ntl, 0);
-        grid = update_grid(s, (const void*)fn, 0);
-        form = 0;
+    int form = g_block_form == 4 || g_block_form == 5 ? g_block_form
+                                                      : (P > kSweepRegMaxP ? 5 : 4);
+    int grid = 0;
+    if (form == 4) {
+        // 5 blocks per CU (all resident at 80 VGPRs), 827-882 vs 855-901 us per 10-pivot sweep
+        // at 16384^2 over 7 (profiles/r03/bpc_ab.jsonl); the wave count must be a multiple of the
+        // chunks per row (update_grid trims it when it can)
+        grid = update_grid(s, (const void*)blk_sweep_fn(P, 4), 0, 5);
+        if (((int64_t)grid * kUpdWaves) % nchunks != 0) form = 5;
     }
+    if (form == 5)   // 8 blocks per CU (P = 16-24 at 64-96 VGPRs, profiles/r04b/lab2.jsonl)
+        grid = sweep_grid_lds(s, 8);
+    BlkSweepFn fn = blk_sweep_fn(P, form);
     BlkHdr* hs = reinterpret_cast<BlkHdr*>(blk);
     const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk + kBlkHdrBytes * slot);
     const double* mul = reinterpret_cast<const double*>(blk + L.mul + slot * L.mul_slot);
     const double* pr = reinterpret_cast<const double*>(blk + L.pr + slot * L.pr_slot);
-    // SMX_BLK_LDSPAD (experiments): dynamic LDS per sweep workgroup, to cap resident blocks
-    static const int ldspad_env = [] {
-        const char* e = getenv("SMX_BLK_LDSPAD");
-        return e ? atoi(e) : 0;
-    }();
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), (size_t)ldspad_env, st, tin, tother,
-                       s.ld, s.rows + 1, s.m + 1, h, mul, pr, hs, ipx, in_idx);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kUpdBlock), 0, st, tin, tother, s.ld, s.rows + 1,
+                       s.m + 1, h, mul, pr, hs, ipx, in_idx);
     // the flag form's pivot columns, or a block cut short by a terminal outcome (does nothing
     // otherwise)
-    if (P > 1 || form == 4)
-        hipLaunchKernelGGL(k_blk_sweep_rest, dim3(num_cus() * 2), dim3(kUpdBlock), 0, st, tin,
-                           tother, s.ld, s.rows + 1, s.m + 1, P, h, mul, pr, hs, ipx_part,
-                           in_idx, form == 4 ? 1 : 0, ipx);
+    hipLaunchKernelGGL(k_blk_sweep_rest, dim3(num_cus() * 2), dim3(kUpdBlock), 0, st, tin,
+                       tother, s.ld, s.rows + 1, s.m + 1, P, h, mul, pr, hs, ipx_part, in_idx, 1,
+                       ipx);
     return (int)hipGetLastError();
 }
 
@@ -1524,6 +1489,12 @@ int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t coun
     hipLaunchKernelGGL(k_fastdiv_bounded_check, dim3(1024), dim3(256), 0, S(stream), num, den,
                        count, out);
     return (int)hipGetLastError();
+}
+
+int smx_tune_block_form(int32_t form) {
+    const int prev = g_block_form;
+    if (form == 0 || form == 4 || form == 5) g_block_form = form;
+    return prev;
 }
 
 int smx_tune_block_pipe(int32_t on) {

@@ -65,7 +65,7 @@ EXPORTS = (
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
     "smx_tune_resident", "smx_tune_resident_timeout", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check", "smx_fastdiv_check_bounded",
-    "smx_tune_block", "smx_tune_block_pipe", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
+    "smx_tune_block", "smx_tune_block_pipe", "smx_tune_block_form", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_graph_create",
@@ -146,6 +146,7 @@ def load():
         "smx_fastdiv_check_bounded": ([vp, vp, i64, vp, vp], ctypes.c_int),
         "smx_tune_block": ([i32], ctypes.c_int),
         "smx_tune_block_pipe": ([i32], ctypes.c_int),
+        "smx_tune_block_form": ([i32], ctypes.c_int),
         "smx_block_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
         "smx_block_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp],
                           ctypes.c_int),
@@ -234,6 +235,12 @@ def tune_block(pivots: int = -1) -> int:
     return int(load().smx_tune_block(pivots))
 
 
+def tune_block_form(form: int = -1) -> int:
+    """smx_tune_block_form: 0 automatic, 4 pivot-row slices in registers, 5 in LDS; any other
+    value only queries; returns the previous setting."""
+    return int(load().smx_tune_block_form(form))
+
+
 def tune_block_pipe(on: int = -1) -> int:
     """smx_tune_block_pipe: 0 plan every block on the solver stream (the default), 1 plan the
     next block on a second stream during each sweep (opt-in), -1 query only; returns the previous
@@ -248,7 +255,7 @@ def tune_shard_xchg(mode: int = -2) -> int:
     return int(load().smx_tune_shard_xchg(mode))
 
 
-BLOCK_MAX = 16   # pivots per sweep at most (kBlkMax)
+BLOCK_MAX = 24   # pivots per sweep at most (kBlkMax)
 
 
 RESIDENT_TIMEOUT = 1   # smx_ctl.dec[0][0] after a resident hand-off timed out

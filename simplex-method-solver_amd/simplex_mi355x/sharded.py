@@ -330,7 +330,9 @@ class BlockShardBackend:
         """run_native's chain of k pivots captured as a hipGraph (smx_bshard_graph_create), for
         the current parity; cached per (parity, k, comm)."""
         d = self.dev
-        key = (d.step & 1, int(k), comm.handle)
+        # the exchange form is baked in at capture time, and a communicator handle can be reused
+        # after close: key on both (close() / drop_graphs() free the cache)
+        key = (d.step & 1, int(k), id(comm), comm.handle, _lib.tune_shard_xchg(-2))
         graphs = self.__dict__.setdefault("_graphs", {})
         if key not in graphs:
             h = ctypes.c_void_p()
@@ -353,6 +355,10 @@ class BlockShardBackend:
     def drop_graphs(self) -> None:
         for g in self.__dict__.pop("_graphs", {}).values():
             g.destroy()
+
+    def close(self) -> None:
+        """Free the captured chains (they hold the communicator they were captured with)."""
+        self.drop_graphs()
 
     def run_native_timed(self, k: int, comm: "RcclComm"):
         """Like run_native, with HIP events around every sweep (synchronous)."""
@@ -381,6 +387,16 @@ class BlockShardBackend:
 
     def local_table(self) -> np.ndarray:
         return self.dev.download()
+
+
+def rank_block_pivots(rows: int, m: int) -> int:
+    """Pivots per sweep on one rank's row block: the single-GPU policy (smx_block_bytes, i.e.
+    block_pivots in libsmx) applied to an unsharded table of the rank's size; 8 where that policy
+    would not use blocks (a small rank table still saves sweeps at 8)."""
+    ld = -(-(m + 1) // 16) * 16
+    shape = [ld, rows, rows, m, m, 0, _lib.load().smx_nparts_for(rows, m)]
+    plan = _lib.block_plan(shape, 0) if rows >= 1 else None
+    return plan[1] if plan is not None else 8
 
 
 def run_block_protocol(be, k: int, exchange, pivots: int | None = None, reduce_row=None,
@@ -506,11 +522,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     local[-1, :m] = lp.objective(args.kind, args.seed, m)
     pivots = getattr(args, "pivots", None)
     if pivots is None:
-        # the unsharded policy on the rank's own table: 12 pivots per sweep from 1 GiB, 10 from
-        # 256 MiB, else 8 (a sweep of 8 costs little more than one of 2 once the table is big)
-        ld = -(-(m + 1) // 16) * 16
-        rank_bytes = (hi - lo + 1) * ld * 8
-        pivots = 12 if rank_bytes >= (1 << 30) else (10 if rank_bytes >= (256 << 20) else 8)
+        pivots = rank_block_pivots(hi - lo, m)
     pivots = int(pivots or 1)
     block = pivots > 1
     xmode = {"auto": -1, "full": 0, "light": 1}[getattr(args, "xchg", "auto") or "auto"]
@@ -559,7 +571,14 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     mn = stats.clone()
     dist.all_reduce(mn, op=dist.ReduceOp.MIN)
     wall = float(mx[0])
-    enqueue = _enqueue_probe(be, comm, args.steps) if block else None
+    enqueue = None
+    if block and getattr(args, "enqueue_probe", False):
+        # opt-in (it captures RCCL graphs and runs ~7x --steps more pivots after the timed
+        # region): a failure is recorded in the line instead of losing the metric
+        try:
+            enqueue = _enqueue_probe(be, comm, args.steps)
+        except Exception as exc:   # noqa: BLE001 -- reported, not raised
+            enqueue = {"error": f"{type(exc).__name__}: {exc}"}
     local_bytes = 16.0 * (hi - lo + 1) * C
     ld = be.dev.ld
     # bytes each rank receives per pivot: full = every rank's slot (8 + 2 ld doubles); light =
@@ -618,6 +637,8 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
         }
         print(json.dumps(out), flush=True)
     dist.barrier()
+    if block:
+        be.close()   # captured chains reference comm: free them before it
     comm.close()
     dist.destroy_process_group()
 

@@ -1,7 +1,8 @@
 """GPU parity of block pivots (smx_block_run, csrc/smx_block.hpp): P pivots planned from the
 block's input table and applied in one HBM sweep.  Bit-exact against the golden fixtures, the C
-oracle and the one-pivot-per-sweep chain, for block sizes 1..16, ragged last blocks,
-terminal outcomes inside a block, the x-history ring and interleaving with host steps.
+oracle and the one-pivot-per-sweep chain, for block sizes 1..24, both sweep layouts (pivot-row
+slices in registers / in LDS, smx_tune_block_form), ragged last blocks, terminal outcomes inside
+a block, the x-history ring and interleaving with host steps.
 """
 from __future__ import annotations
 
@@ -33,6 +34,15 @@ def block_mode():
     _lib.tune_resident(prev_r)
 
 
+@pytest.fixture
+def sweep_form():
+    """Set smx_tune_block_form (sweep layout 0 auto / 4 registers / 5 LDS) for one test."""
+    from simplex_mi355x import _lib
+    prev = _lib.tune_block_form(-1)
+    yield _lib.tune_block_form
+    _lib.tune_block_form(prev)
+
+
 CASES = list(trajectory_cases())
 
 
@@ -45,10 +55,12 @@ def _solve(cons, func, cap, chunk):
                 table_hash(last.table))
 
 
-@pytest.mark.parametrize("P", [2, 3, 4, 8, 11, 16])
-def test_every_fixture_block_vs_chain_vs_reference(block_mode, P):
+@pytest.mark.parametrize("P,form", [(2, 0), (3, 5), (4, 0), (8, 0), (8, 5), (11, 0), (16, 0),
+                                    (16, 4), (20, 0), (24, 5)])
+def test_every_fixture_block_vs_chain_vs_reference(block_mode, sweep_form, P, form):
     """Every trajectory fixture: block chain == one-pivot chain == the reference's pivots, with
     chunks that end inside and at block boundaries and terminal outcomes inside blocks."""
+    sweep_form(form)
     n_blk = 0
     for label, cons, func, rec in CASES:
         if len(func) not in (len(cons[0]) - 1, len(cons[0])) or len(func) < 2:
@@ -81,11 +93,19 @@ def test_every_fixture_block_vs_chain_vs_reference(block_mode, P):
     ("uniform", 2047, 2047, 100, 100, 16),     # 16 pivots per sweep, ragged last block
     ("mixed", 1500, 1100, 160, 80, 13),
     ("degenerate", 700, 700, 200, 200, 12),
+    ("uniform", 2047, 2047, 110, 110, 20),     # LDS layout from 13 pivots on
+    ("mixed", 1500, 1100, 160, 80, 24),
+    ("degenerate_mixed", 900, 1300, 150, 75, 22),
+    ("uniform", 255, 65535, 48, 48, 24),       # 512 chunks per row: one workgroup each
 ])
-def test_block_vs_oracle(block_mode, kind, n, m, k, chunk, P):
+@pytest.mark.parametrize("form", [0, 4, 5])
+def test_block_vs_oracle(block_mode, sweep_form, kind, n, m, k, chunk, P, form):
     from oracle import c_oracle
     from simplex_mi355x import lp
     import simplex
+    if form == 4 and P > 16:
+        pytest.skip("register layout: up to 16 pivots tested")
+    sweep_form(form)
     block_mode(P)
     T = lp.dense_tableau(kind, 11, n, m)
     sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
@@ -99,8 +119,9 @@ def test_block_vs_oracle(block_mode, kind, n, m, k, chunk, P):
     assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
 
 
-@pytest.mark.parametrize("P", [10, 12, 16])
-def test_block_bounded_fast_path_edges_vs_oracle(block_mode, P):
+@pytest.mark.parametrize("P", [10, 12, 16, 20, 24])
+@pytest.mark.parametrize("form", [4, 5])
+def test_block_bounded_fast_path_edges_vs_oracle(block_mode, sweep_form, P, form):
     """The one-row sweep's unchecked fast path (smx_block.hpp, kBndSpan) next to its fallbacks in
     one table: rows scaled past 2^101 (input bound), rows scaled to ~2^-60 (small numerators),
     columns scaled to ~2^-99 (pivot-row values below 2^-100: the chunk falls back), exact zeros
@@ -108,6 +129,7 @@ def test_block_bounded_fast_path_edges_vs_oracle(block_mode, P):
     from oracle import c_oracle
     from simplex_mi355x import lp
     import simplex
+    sweep_form(form)
     block_mode(P)
     n = m = 1023
     T = lp.dense_tableau("uniform", 5, n, m)
@@ -252,8 +274,8 @@ def test_block_plan_policy(block_mode):
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4]) is None
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 6)[1] == 6
     assert _lib.block_plan([1024, 100, 1023, 1023, 1023, 0, 4], 4) is None  # sharded
-    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 16)[1] == 16
-    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 17) is None
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 24)[1] == 24
+    assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 25) is None
     block_mode(1)
     assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64]) is None
 
