@@ -478,6 +478,24 @@ int smx_host_pivot(const double* Tin, double* Tout, const smx_shape* shape, int3
 int64_t smx_host_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity,
                      int64_t k, int32_t* log, int32_t* status_out);
 
+/* ---- Integer inputs: the first pivot's zero signs (smx_intfirst.hpp) ------------------------
+ * The reference holds the caller's Python ints as ints until its first recalculate_matrix
+ * (simplex.py:36-39, :155-175), and int arithmetic gives some zero results of that pivot the
+ * opposite sign from fp64 (-0 is the int 0; an int product 0 * -3 is +0).  After the regular
+ * first pivot T0 -> T1 (any engine: update, block, resident, sharded), this rewrites the entries
+ * of T1 that are +-0 with the int semantics; every other entry already agrees in every bit
+ * (|ints| < 2^26).  rows x cols local entries (ld doubles per row), r_local = the pivot row's
+ * local index or -1 when another rank holds it, prow = T0's pivot row (cols doubles, e =
+ * prow[c]), mask = 1 byte per T0 entry (ldm per row; nonzero = the caller passed an int) or
+ * NULL when every entry is an int, maskr = the pivot row's mask (NULL likewise).  Device
+ * pointers and `stream` for smx_int_first_fix, host pointers (synchronous) for the host form. */
+int smx_int_first_fix(const double* T0, double* T1, int64_t ld, int32_t rows, int32_t cols,
+                      int32_t r_local, int32_t c, const double* prow, const uint8_t* mask,
+                      int64_t ldm, const uint8_t* maskr, void* stream);
+int smx_host_int_first_fix(const double* T0, double* T1, int64_t ld, int32_t rows, int32_t cols,
+                           int32_t r_local, int32_t c, const double* prow, const uint8_t* mask,
+                           int64_t ldm, const uint8_t* maskr);
+
 #ifdef __cplusplus
 }
 #endif

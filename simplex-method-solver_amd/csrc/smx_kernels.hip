@@ -51,6 +51,7 @@ static_assert(sizeof(smx_part) == 32, "smx_part layout");
 #include "smx_resident.hpp"
 #include "smx_block.hpp"
 #include "smx_host.hpp"
+#include "smx_intfirst.hpp"
 
 namespace {
 
@@ -1896,6 +1897,25 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
     delete[] bp;
     (void)hipSetDevice(dev0);
     return err;
+}
+
+int smx_int_first_fix(const double* T0, double* T1, int64_t ld, int32_t rows, int32_t cols,
+                      int32_t r_local, int32_t c, const double* prow, const uint8_t* mask,
+                      int64_t ldm, const uint8_t* maskr, void* stream) {
+    if (!int_first_args_ok(T0, T1, ld, rows, cols, r_local, c, prow, mask, ldm))
+        return (int)hipErrorInvalidValue;
+    const int grid = rows < 4096 ? rows : 4096;
+    hipLaunchKernelGGL(k_int_first_fix, dim3(grid), dim3(256), 0, S(stream), T0, T1, ld, rows,
+                       cols, r_local, c, prow, mask, ldm, maskr);
+    return (int)hipGetLastError();
+}
+
+int smx_host_int_first_fix(const double* T0, double* T1, int64_t ld, int32_t rows, int32_t cols,
+                           int32_t r_local, int32_t c, const double* prow, const uint8_t* mask,
+                           int64_t ldm, const uint8_t* maskr) {
+    if (!int_first_args_ok(T0, T1, ld, rows, cols, r_local, c, prow, mask, ldm)) return -1;
+    host_int_first_fix(T0, T1, ld, rows, cols, r_local, c, prow, mask, ldm, maskr);
+    return 0;
 }
 
 }  // extern "C"

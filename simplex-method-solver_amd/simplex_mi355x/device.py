@@ -56,6 +56,32 @@ class Graph:
             self.handle = None
 
 
+def int_first_fix(T0: torch.Tensor, T1: torch.Tensor, C: int, mask, r: int, c: int,
+                  prow: torch.Tensor | None = None, maskr=None) -> None:
+    """The int semantics of the zero results of a table's first pivot T0 -> T1
+    (``smx_int_first_fix``, csrc/smx_intfirst.hpp; simplex.py:155-175 on the caller's ints), on
+    the current stream.  ``T0`` / ``T1``: ``float64[rows][ld]`` on one device; ``mask``: uint8
+    ``[rows][C]`` host array (nonzero = the caller passed an int there) or None when every entry
+    is an int; ``r``: the local pivot row (-1: held by another rank, whose T0 row is ``prow``);
+    ``maskr``: the pivot row's mask when it is not a row of ``mask``."""
+    rows, ld = int(T0.shape[0]), int(T0.shape[1])
+    dev = T0.device
+    if prow is None:
+        prow = T0[r]
+    md = mr = None
+    if mask is not None:
+        md = torch.from_numpy(np.ascontiguousarray(mask, dtype=np.uint8)).to(dev)
+        if maskr is None:
+            mr = md[r]
+    if maskr is not None:
+        mr = torch.from_numpy(np.ascontiguousarray(maskr, dtype=np.uint8)).to(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    _lib.check(_lib.load().smx_int_first_fix(
+        T0.data_ptr(), T1.data_ptr(), ld, rows, int(C), int(r), int(c), prow.data_ptr(),
+        None if md is None else md.data_ptr(), int(C), None if mr is None else mr.data_ptr(),
+        stream), "smx_int_first_fix")
+
+
 class DeviceTableau:
     """A dense fp64 tableau in HBM plus the state of the pivot loop."""
 
@@ -433,6 +459,15 @@ class DeviceTableau:
         with torch.cuda.stream(self.stream):
             ops.update_forced(self.buf[p], self.buf[p ^ 1], self.shape, r, c)
         self.step += 1
+
+    def int_first_fix(self, mask, r: int, c: int, prow: torch.Tensor | None = None,
+                      maskr=None) -> None:
+        """After the table's first pivot (buf[(step - 1) & 1] -> buf[step & 1]): the int
+        semantics of its zero results (see :func:`int_first_fix`).  ``r``: local pivot row."""
+        self.settle()
+        p0 = (self.step - 1) & 1
+        with torch.cuda.stream(self.stream):
+            int_first_fix(self.buf[p0], self.buf[p0 ^ 1], self.C, mask, r, c, prow, maskr)
 
     def close(self) -> None:
         for g in self._graphs.values():

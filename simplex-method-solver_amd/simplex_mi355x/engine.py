@@ -17,8 +17,13 @@ Additions (not in the reference, all opt-in): ``step()`` (one pick + pivot), ``s
 Deliberate differences, all on inputs the reference UI never produces (main.py:309-312 always
 passes rectangular float rows and ``len(function) == m``):
 * ragged constraint rows raise ``ValueError`` (the device tableau is dense);
-* integer inputs are held as fp64 on the device; integer arithmetic in the reference can differ
-  only in the sign of a zero on the first pivot, which no comparison in the rules can see.
+* integer inputs are held as fp64 on the device.  The reference keeps them as Python ints until
+  its first pivot, whose int arithmetic gives some zero results the opposite sign from fp64
+  (-0 is the int 0; an int product 0 * -3 is +0): the first pivot of a table with int entries
+  is followed by ``smx_int_first_fix`` (csrc/smx_intfirst.hpp), which rewrites exactly those
+  zeros, so the tables match the reference's bits (tests/golden/intzero.json).  That holds
+  while every int is below 2^26 in magnitude (products and differences exact in fp64); larger
+  ints get a ``RuntimeWarning``: the reference computes their products exactly, fp64 rounds.
 """
 from __future__ import annotations
 
@@ -153,10 +158,14 @@ class History:
             sc = self._scratch
             sc[0].copy_(self.ckpt[s0])
             from . import ops
+            ih = self.sm._int_hist
             for t in range(s0, step):
                 a = (t - s0) & 1
                 r, c = log[t]
                 ops.update_forced(sc[a], sc[a ^ 1], dev.shape, r, c)
+                if t == 0 and ih is not None:   # the caller's ints: their first pivot's zeros
+                    from .device import int_first_fix
+                    int_first_fix(sc[a], sc[a ^ 1], dev.C, ih[0], ih[1], ih[2])
             T = sc[(step - s0) & 1][:, :dev.C].cpu().numpy()
         rows = T[:self.sm.n].tolist()
         rows.append(T[self.sm.n, :min(self.sm.flen, self.sm.m + 1)].tolist())
@@ -172,6 +181,47 @@ def _dense_from_lists(constraints, function, m):
     if k:
         T[n, :k] = np.asarray(function[:k], dtype=np.float64)
     return T
+
+
+INT_EXACT = 1 << 26   # |int| below this: the first pivot's int products are exact in fp64
+
+
+def _int_entries(constraints, function, m, dense):
+    """Which tableau entries the caller passed as ints (Python ``int`` / ``bool``, numpy integer
+    scalars or integer rows): None when none, True when all of them, else a uint8 mask
+    ``[n + 1][m + 1]``."""
+    rows = list(constraints) + [function]
+    n = len(constraints)
+    kinds = []
+    for row in rows:
+        if isinstance(row, np.ndarray):
+            kinds.append(1 if row.dtype.kind in "iub" else 0)
+            continue
+        ts = set(map(type, row))
+        ints = {t for t in ts if issubclass(t, (int, np.integer))}
+        kinds.append(0 if not ints else (1 if ints == ts else 2))
+    if not any(kinds):
+        return None
+    if all(k == 1 for k in kinds):   # (f-row padding is never an operand: int or not alike)
+        mask = True
+        big = float(np.abs(dense[:n + 1, :m + 1]).max(initial=0.0)) >= INT_EXACT
+    else:
+        mask = np.zeros((n + 1, m + 1), dtype=np.uint8)
+        for i, (row, k) in enumerate(zip(rows, kinds)):
+            if k == 1:
+                mask[i, :min(len(row), m + 1)] = 1
+            elif k == 2:
+                mask[i, :min(len(row), m + 1)] = [isinstance(x, (int, np.integer))
+                                                  for x in row[:m + 1]]
+        big = float(np.abs(np.where(mask != 0, dense[:n + 1, :m + 1], 0.0)).max(initial=0.0)) \
+            >= INT_EXACT
+    if big:
+        import warnings
+        warnings.warn("simplex_mi355x: integer inputs of magnitude >= 2^26: the reference forms "
+                      "their first-pivot products in exact integer arithmetic, this engine in "
+                      "fp64 (the results may differ in the last bits)", RuntimeWarning,
+                      stacklevel=3)
+    return mask
 
 
 def _use_host(device) -> bool:
@@ -230,6 +280,10 @@ class SimplexMethod:
         else:
             self._dev = DeviceTableau(dense, self.n, self.m, self.flen, device=device)
         self._pristine = True
+        # int entries of the caller's table (None / True / mask): pending until the first pivot,
+        # then kept with its (r, c) for history replays (_int_first_fix)
+        self._int0 = _int_entries(constraints, function, self.m, dense)
+        self._int_hist = None
         self.pivot_log: list[tuple[int, int]] = []
         self.status = "ready"
         self.cycle = None          # (first step of a repeated basis, period) when detected
@@ -258,6 +312,7 @@ class SimplexMethod:
         self._initial = None
         self._dev = dev
         self._pristine = False
+        self._int0 = self._int_hist = None
         self.pivot_log = []
         self.status = "ready"
         self.cycle = None
@@ -290,8 +345,11 @@ class SimplexMethod:
             raise ValueError("table shape does not match this problem")
         self._initial = list(value)
         self.flen = len(func)
-        self._dev.upload(_dense_from_lists(cons, func, self.m))
+        dense = _dense_from_lists(cons, func, self.m)
+        self._dev.upload(dense)
         self._pristine = True
+        self._int0 = _int_entries(cons, func, self.m, dense)
+        self._int_hist = None
 
     @property
     def backend(self) -> str:
@@ -365,9 +423,29 @@ class SimplexMethod:
         if self.flen > self.m + 1 or (self.flen < self.m and c >= self.flen):
             # the reference's step 2 / step 4 index the f-row out of range (simplex.py:159-175)
             raise IndexError("list index out of range")
+        first_int = self._pristine and self._int0 is not None
         self._dev.apply_selected()
+        if first_int:
+            self._int_first_fix(r, c)
         self._pristine = False
         self.pivot_log.append((r, c))
+
+    def _int_first_fix(self, r, c):
+        """The first pivot of a table with int entries just ran (r, c): give its zero results
+        the signs the reference's int arithmetic gives them (smx_int_first_fix)."""
+        mask = None if self._int0 is True else self._int0
+        self._dev.int_first_fix(mask, r, c)
+        self._int_hist = (mask, r, c)
+        self._int0 = None
+
+    def _int_first_after_run(self, before, done):
+        """After a chained run that began at the caller's table: the int fix of its first pivot
+        (the chained loops run that pivot alone while one is pending).  True when applied."""
+        if self._int0 is None or before != 0 or done < 1 or not self._pristine:
+            return False
+        r, c = (int(x) for x in self._dev.read_log(0, 1)[0])
+        self._int_first_fix(r, c)
+        return True
 
     def recalculate_matrix(self):
         """simplex.py:143-177."""
@@ -453,10 +531,13 @@ class SimplexMethod:
         status = None
         while self.pivots - start < budget:
             k = int(min(chunk, budget - (self.pivots - start), dev.log_cap))
+            if self._int0 is not None and self._pristine:
+                k = 1                      # the first pivot of an int table runs alone
             before = dev.step
             dev.run(k, graph=(k == chunk))
             ctl = dev.sync_state()
             done = int(ctl["npivots"])
+            fixed = self._int_first_after_run(before, done)
             logs = dev.read_log(before, done)
             xs = dev.read_xhist(before, done)
             cycled = False
@@ -466,8 +547,12 @@ class SimplexMethod:
                 self.row[c], self.column[r] = self.column[r], self.row[c]   # simplex.py:152
                 self.pivot_log.append((r, c))
                 self._pristine = False
-                x1 = float(v1) if 'x1' in self.column else 0                # simplex.py:51-68
-                x2 = float(v2) if 'x2' in self.column else 0
+                if fixed:                  # the ring holds the pre-fix values of pivot 0
+                    x1, x2 = self.find_optimum()
+                    fixed = False
+                else:
+                    x1 = float(v1) if 'x1' in self.column else 0            # simplex.py:51-68
+                    x2 = float(v2) if 'x2' in self.column else 0
                 result.append(LazyInfo(self.row, self.column, hist, self.pivots, None, None,
                                        x1, x2, self.f(x1, x2)))
                 cycled = self._track(r, c, detect_cycles) or cycled   # stop after this chunk
@@ -519,10 +604,13 @@ class SimplexMethod:
         status = None
         while self.pivots - start < budget:
             k = int(min(chunk, budget - (self.pivots - start), dev.log_cap))
+            if self._int0 is not None and self._pristine:
+                k = 1                      # the first pivot of an int table runs alone
             before = dev.step
             dev.run(k, graph=graph and k == chunk)
             ctl = dev.sync_state()
             done = int(ctl["npivots"])
+            self._int_first_after_run(before, done)
             cycled = False
             for r, c in dev.read_log(before, done):
                 r, c = int(r), int(c)

@@ -124,6 +124,17 @@ class HostTableau:
         self._term = self._status != _lib.IDLE
         self._sel = None
 
+    def int_first_fix(self, mask, r: int, c: int) -> None:
+        """After the table's first pivot: the int semantics of its zero results
+        (``smx_host_int_first_fix``, csrc/smx_intfirst.hpp; simplex.py:155-175 on ints)."""
+        p0 = (self.step - 1) & 1
+        md = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        T0 = self.buf[p0]
+        _lib.check(self._L.smx_host_int_first_fix(
+            self._ptr(T0), self._ptr(self.buf[p0 ^ 1]), self.ld, self.n + 1, self.C, r, c,
+            self._ptr(T0[r]), None if md is None else self._ptr(md), self.C,
+            None if md is None else self._ptr(md[r])), "smx_host_int_first_fix")
+
     def sync_state(self) -> dict:
         return {"npivots": self.step, "term": self._term, "sel_status": self._status}
 

@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .device import int_first_fix
 from .sharded import BlockShardBackend, row_range
 
 
@@ -282,6 +283,25 @@ class MultiTableau:
                 be.publish(parity ^ 1, 1)
         self._saved = None
         self.step += 1
+
+    def int_first_fix(self, mask, r: int, c: int) -> None:
+        """After the table's first pivot: the int semantics of its zero results on every rank
+        (smx_int_first_fix with T0's pivot row copied from its owner; simplex.py:155-175)."""
+        self._sync()
+        p0 = (self.step - 1) & 1
+        owner, rl = self._owner(r)
+        src = self.ranks[owner].dev.buf[p0][rl]
+        n = self.n
+        for q, be in enumerate(self.ranks):
+            lo, hi = self.ranges[q]
+            d = be.dev
+            local = None if mask is None else np.concatenate([mask[lo:hi], mask[n:n + 1]])
+            with torch.cuda.device(d.device), be.stream_ctx():
+                prow = src.to(d.device)
+                int_first_fix(d.buf[p0], d.buf[p0 ^ 1], self.C, local,
+                              rl if q == owner else -1, c, prow,
+                              None if mask is None else mask[r])
+        self._sync()
 
     def forced(self, r: int, c: int) -> None:
         raise NotImplementedError("forced pivots are a single-device microbenchmark")
