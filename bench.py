@@ -5,17 +5,21 @@ tableau (n = m = 16383; seeded uniform random LP A~U(-1,1), b~U(0.1,1), c~U(-1,1
 the origin so the trajectory is a long phase-2 run), resident in HBM before timing starts.
 A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): its selection
 (pick_element, :70-141) and its Jordan step over every element (recalculate_matrix, :143-177).
-At N = 1 on this table the steps run as block pivots: 8 pivots are decided by one planner launch
-each (k_blk_step, every value of the intermediate tables re-derived from the block's input with
-the update's own expression) and applied by ONE sweep of the tableau (k_blk_sweep), so a sweep
-moves 16 B per element for 8 pivots; bit-identical to one pivot per sweep.  The one-pivot chain
+At N = 1 on this table the steps run as block pivots: up to P pivots (the library's policy,
+smx_tune_block: 12 for tables of 256 MiB and more) are decided by one planner launch each
+(k_blk_step, every value of the intermediate tables re-derived from the block's input with the
+update's own expression) and applied by ONE sweep of the tableau (k_blk_sweep), so a sweep moves
+16 B per element for P pivots (a chain of k pivots is cut into blocks of near-equal size: 20
+pivots are two sweeps of 10); bit-identical to one pivot per sweep.  The one-pivot chain
 (k_update<kFused>, one kernel per pivot) is timed beside it as "single_pivot_update".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size S]
 
 N = 1: one process.  N > 1: launched by torch.distributed.run, one rank per GPU; the tableau's
-constraint rows are block-partitioned (strong scaling of the same tableau) and every pivot
-exchanges one all-gather of (header + candidate rows) over RCCL.  Timing: barrier +
+constraint rows are block-partitioned (strong scaling of the same tableau) and run the
+block-sharded chain (sharded.py, smx_bshard_*): every pivot of a block exchanges one all-gather
+of (header + candidate rows) over RCCL -- from 4 ranks on the light form, an all-gather of the
+headers plus one max all-reduce of the pivot row -- and each rank sweeps its rows once per block.  Timing: barrier +
 synchronize on both sides of exactly K pivots, max over ranks.  Rank 0 prints ONE JSON line.
 
 roofline: algorithmic bytes of the dominant kernel = 16 B per tableau element per launch

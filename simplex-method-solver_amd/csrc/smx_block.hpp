@@ -691,6 +691,11 @@ __device__ unsigned g_blk_fallback[kBlkMax + 1][2];
     } while (0)
 #endif
 
+// The f-row of step parity sp (fr [2][ld], blk_step_body)
+__device__ __forceinline__ const double* fo_of(const double* fr, int sp, int64_t ld) {
+    return fr + (int64_t)sp * ld;
+}
+
 // One pivot of the block: decide block step D = L-1 and build the records of step L.
 // SH = false: the decision from the records of step D and the pivot-row values derived on the
 // fly; SH = true (row-sharded): from the P gathered send slots in `recv` (merge_headers), the
@@ -754,6 +759,69 @@ __device__ __forceinline__ bool blk_step_body(
     } else {
         blk_load_pivots(h, D, &s_pv);
     }
+    // Operands of the phase-2 pivot-row chains and of the row pass that do not depend on the
+    // decision, issued before it so their latency hides under the records' round trip (the
+    // phase-2 step's loads after the decision were 3(D + 2) per thread and that phase grew
+    // from 1.3 to 4.5 us per step with D, profiles/r03b/planner_trace_P10_dpp_mulT.jsonl): the
+    // f-row of T_{k+D} and the pivot rows pr_q at this thread's phase-2 columns (c0 = the column
+    // the records of step D were built on, which is the entering column in phase 2; m; its slice
+    // column; its first-round scan columns), and its first row's multipliers and cached columns.
+    // Nothing is pinned here (a pin would wait for the load); phase 1 discards them.
+    constexpr int NSC = NT >= 128 ? 1 : 128 / NT;   // first-round scan columns per thread
+    constexpr int NJ = 2 + NSC;   // c or m (by lane parity), slice, scan columns
+    int jj[NJ];
+    double fv[NJ], pq[NJ][kBlkMax];
+    double pmq[kBlkMax], pxb = 0.0, pxc = 0.0;
+    const int i0 = b * NT + tid;
+    // The row pass reads T_k[i][cf] (and T_k[i][c] at step 0) for its rows: one 8-B load per row,
+    // each a different DRAM page.  The entering column is nearly always among the first columns
+    // (uniform LPs at 4096^2: median 6, 99.3 % below 32 over 300 pivots), so the first kWin
+    // columns of this thread's first row are staged in LDS at entry, beside the prefetches
+    // above, and the row pass reads its column from there when it falls inside.
+    constexpr int kWin = 32;
+    __shared__ double s_win[(SH || LAG) ? 1 : NT * kWin];
+    const bool use_win = !SH && !LAG && C >= kWin && b * NT < rows;
+    const int c0 = SH || LAG ? 0 : hs->cfs[blk_slot(D, P, bn)];
+    if constexpr (!SH && !LAG) {
+        const int S = ((C + G - 1) / G + 1) & ~1;
+        jj[0] = (tid & 1) ? m : c0;
+        jj[1] = b * S + tid;
+#pragma unroll
+        for (int k = 0; k < NSC; ++k) jj[2 + k] = tid + k * NT;
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+            const int jc = min(jj[u], C - 1);
+            fv[u] = fo_of(fr, sp, ld)[jc];
+#pragma unroll
+            for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
+        }
+        if (use_win) {
+            // LDS-DMA: each wave loads the window of its own 64 rows (no VGPRs, no barrier; the
+            // row pass waits for vmcnt before its one read)
+            const int w = tid >> 6, lane = tid & (kWave - 1);
+            constexpr int LPR = kWin / 2;          // lanes per row (16 B each)
+            constexpr int RPI = kWave / LPR;       // rows per wave-instruction
+#pragma unroll
+            for (int k = 0; k < kWave / RPI; ++k) {
+                const int rw = w * kWave + k * RPI;
+                const int row = min(b * NT + rw + lane / LPR, rows - 1);
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(T + (int64_t)row * ld + (lane % LPR) * 2),
+                    (__attribute__((address_space(3))) void*)(s_win + rw * kWin), 16, 0, 0);
+            }
+        }
+        if (i0 < rows) {
+            const double* mT0 = blk_mulT(mul, rows + 1);
+#pragma unroll
+            for (int q = 0; q < D; ++q) pmq[q] = mT0[(int64_t)q * (rows + 1) + i0];
+            if (D > 0) {
+                const double* colm0 = fr + 2 * ld;
+                const double* cca0 = colm0 + 3 * (int64_t)rows;
+                pxc = cca0[(int64_t)(D & 1) * rows + i0];
+                pxb = cca0[2 * (int64_t)rows + (int64_t)(D & 1) * rows + i0];
+            }
+        }
+    }
     if (SH) {
         if (tid == 0) {
             // full exchange: recv = the gathered send slots; light (xslot = SMX_SHARD_HDR): recv
@@ -769,7 +837,7 @@ __device__ __forceinline__ bool blk_step_body(
         }
     } else if (tid < kWave) {
         // the decision of step D from its records (every workgroup, identically)
-        const int c = hs->cfs[blk_slot(D, P, bn)];
+        const int c = LAG ? hs->cfs[blk_slot(D, P, bn)] : c0;
         int nb;
         First f;
         Cand bb;
@@ -881,26 +949,13 @@ __device__ __forceinline__ bool blk_step_body(
     // columns cost 7 chains and 7 (D + 2) loads per thread on every step: tools/trace_planner.hip,
     // profiles/r03b/).  Same chains on the same operands: the same values.
     if (!SH && !LAG && nb == SMX_NONE) {
-        c = d.c;
+        c = d.c;                       // == c0: the prefetched columns are this step's
         const double* Tr = T + (int64_t)r_local * ld;
         const int S = ((C + G - 1) / G + 1) & ~1;
         const int s0 = b * S, s1 = min(C, s0 + S);
-        constexpr int NSC = NT >= 128 ? 1 : 128 / NT;   // first-round scan columns per thread
-        constexpr int NJ = 2 + NSC;   // c or m (by lane parity), slice, scan columns
-        int jj[NJ];
-        jj[0] = (tid & 1) ? m : c;
-        jj[1] = s0 + tid;
+        double x[NJ];
 #pragma unroll
-        for (int k = 0; k < NSC; ++k) jj[2 + k] = tid + k * NT;
-        double x[NJ], pq[NJ][kBlkMax], fv[NJ];
-#pragma unroll
-        for (int u = 0; u < NJ; ++u) {
-            const int jc = min(jj[u], C - 1);
-            x[u] = Tr[jc];
-            fv[u] = fo[jc];
-#pragma unroll
-            for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
-        }
+        for (int u = 0; u < NJ; ++u) x[u] = Tr[min(jj[u], C - 1)];
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
             blk_pin(x[u]);
@@ -1153,9 +1208,17 @@ __device__ __forceinline__ bool blk_step_body(
     for (int i = b * NT + tid; i < rows; i += G * NT) {
         const double* row = T + (int64_t)i * ld;
         double* mr = mul + (int64_t)i * kBlkMax;
-        const double xc = reuse_c ? (LAG ? colc : cca)[(int64_t)(D & 1) * rows + i] : row[c];
-        const double xb = D > 0 ? (LAG ? colm[i] : ccb[(int64_t)(D & 1) * rows + i]) : row[m];
-        const double xa = cf != SMX_NONE ? row[cf] : 0.0;
+        const bool pre = !SH && !LAG && i == i0;   // this thread's first row: prefetched at entry
+        const bool win = pre && use_win;
+        if (win) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS-DMA window landed
+        const double xc = reuse_c ? (LAG ? colc[(int64_t)(D & 1) * rows + i]
+                                         : (pre ? pxc : cca[(int64_t)(D & 1) * rows + i]))
+                                  : ((win && c < kWin) ? s_win[tid * kWin + c] : row[c]);
+        const double xb = D > 0 ? (LAG ? colm[i]
+                                       : (pre ? pxb : ccb[(int64_t)(D & 1) * rows + i]))
+                                : row[m];
+        const double xa = cf != SMX_NONE ? ((win && cf < kWin) ? s_win[tid * kWin + cf] : row[cf])
+                                         : 0.0;
         if (LAG && D == 0) colm[i] = xb;
         if (LAG && cf != SMX_NONE) colc[(int64_t)(L & 1) * rows + i] = xa;
         double bv, a;
@@ -1188,7 +1251,7 @@ __device__ __forceinline__ bool blk_step_body(
             double mq[kBlkMax];
             double x3[3] = {xc, xb, xa};
 #pragma unroll
-            for (int q = 0; q < D; ++q) mq[q] = mT[(int64_t)q * (rows + 1) + i];
+            for (int q = 0; q < D; ++q) mq[q] = pre ? pmq[q] : mT[(int64_t)q * (rows + 1) + i];
 #pragma unroll
             for (int q = 0; q < D; ++q) blk_pin(mq[q]);
 #pragma unroll

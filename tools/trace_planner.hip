@@ -86,14 +86,19 @@ int main(int argc, char** argv) {
             CK(hipMemcpyToSymbol(HIP_SYMBOL(g_blk_fallback), zero, sizeof(zero)));
         }
         const int G = s.nparts < kBlkTraceParts ? s.nparts : kBlkTraceParts;
+        unsigned long long prev_end = 0;
         for (int L = 1; L <= P; ++L) {
             unsigned long long t0 = ~0ull, tend = 0;
             for (int g = 0; g < G; ++g) {
                 t0 = std::min(t0, tr[L][g][0]);
                 tend = std::max(tend, tr[L][g][7]);
             }
-            printf("{\"rep\": %d, \"N\": %d, \"P\": %d, \"L\": %d, \"span_us\": %.2f, \"phase_us\": [",
-                   rep, N, P, L, (tend - t0) * 0.01);
+            // gap: this step's first entry after the previous step's last record store
+            const double gap = prev_end ? ((double)t0 - (double)prev_end) * 0.01 : 0.0;
+            prev_end = tend;
+            printf("{\"rep\": %d, \"N\": %d, \"P\": %d, \"L\": %d, \"span_us\": %.2f, "
+                   "\"gap_us\": %.2f, \"phase_us\": [",
+                   rep, N, P, L, (tend - t0) * 0.01, gap);
             for (int ph = 0; ph < 8; ++ph) {
                 std::vector<double> v;
                 for (int g = 0; g < G; ++g) v.push_back((tr[L][g][ph] - t0) * 0.01);
