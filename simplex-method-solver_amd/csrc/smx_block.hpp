@@ -66,8 +66,17 @@ constexpr int kBlkSlots = kBlkMax + 2;   // record / cf slots: steps 1..P-1, and
 constexpr int kBlkNT = kUpdBlock;    // planner workgroup
 constexpr int kBlkScan = 4 * kBlkNT; // columns per early-exit scan round
 constexpr int kBlkPartsPer = kUpdBlock / kBlkNT;
-constexpr int kBlkPartsMax = kMaxParts * kBlkPartsPer;
-__host__ __device__ __forceinline__ int blk_parts_of(int nparts) { return nparts * kBlkPartsPer; }
+// Planner workgroups: the select partition's count (at least one slice of the pivot row per
+// workgroup), raised to one row per thread on tall tables: at 65536 rows 64 workgroups own
+// 1,024 rows each and the row pass runs four rows per thread back to back (config 5's planner
+// took 27.5 us per pivot against 14.4 at 16384^2, profiles/r03c/config5_degenerate_1gpu.json).
+constexpr int kBlkPartsMax = 4 * kMaxParts * kBlkPartsPer;
+__host__ __device__ __forceinline__ int blk_parts_of(int nparts, int rows) {
+    const int by_rows = (rows + kBlkNT - 1) / kBlkNT;
+    int g = nparts * kBlkPartsPer;
+    if (by_rows > g) g = by_rows;
+    return g < kBlkPartsMax ? g : kBlkPartsMax;
+}
 
 // One per plan slot (a pipelined chain alternates two); cfs / loc / np0 are the chain's state and
 // live in slot 0 only (`hs` in the kernels).

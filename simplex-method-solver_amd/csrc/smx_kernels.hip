@@ -501,7 +501,7 @@ struct BlkPtrs {
 };
 BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
     BlkPtrs b;
-    b.L = blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts));
+    b.L = blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts, s.rows));
     for (int k = 0; k < 2; ++k) {
         b.h[k] = reinterpret_cast<BlkHdr*>(blk + kBlkHdrBytes * k);
         b.mul[k] = reinterpret_cast<double*>(blk + b.L.mul + k * b.L.mul_slot);
@@ -517,7 +517,7 @@ int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, s
                      const BlkPtrs& b, hipStream_t st) {
     hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, T, s.ld, s.rows, s.m,
                        fscan_of(s), parity, loc, (const smx_ctl*)ctl, b.h[0], b.h[1], b.fr);
-    hipLaunchKernelGGL(k_blk_first, dim3(blk_parts_of(s.nparts)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
+    hipLaunchKernelGGL(k_blk_first, dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
                        s.row0, (const smx_ctl*)ctl, (const BlkHdr*)b.h[0], b.parts);
     return (int)hipGetLastError();
 }
@@ -531,7 +531,7 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
     BlkStepFn fn = sh ? blk_step_fn_sh<true, false>(L)
                       : (pp > 0 ? blk_step_fn_sh<false, true>(L) : blk_step_fn_sh<false, false>(L));
     const int o = slot ^ 1;
-    hipLaunchKernelGGL(fn, dim3(blk_parts_of(s.nparts)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
+    hipLaunchKernelGGL(fn, dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
                        fscan_of(s), s.row0, P, parity, bn, ctl, b.h[slot], b.h[0], b.parts,
                        b.mul[slot], b.pr[slot], b.fr, recv, nranks, log, xhist, log_cap,
                        (const BlkHdr*)b.h[o], (const double*)b.mul[o], (const double*)b.pr[o],
@@ -558,16 +558,16 @@ int launch_bsh_pick(const double* hdrs, const smx_shape& s, int nranks, int rank
 
 int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
                     const smx_ctl* ctl, const BlkPtrs& b, double* send, hipStream_t st) {
-    hipLaunchKernelGGL(bsh_pack_fn(D), dim3(blk_parts_of(s.nparts)), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
+    hipLaunchKernelGGL(bsh_pack_fn(D), dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
                        s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h[0], (const smx_part*)b.parts,
-                       blk_parts_of(s.nparts), (const double*)b.mul[0], (const double*)b.pr[0], send);
+                       blk_parts_of(s.nparts, s.rows), (const double*)b.mul[0], (const double*)b.pr[0], send);
     return (int)hipGetLastError();
 }
 
 int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, const BlkPtrs& b,
                        hipStream_t st) {
     hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)b.h[0],
-                       (const smx_part*)b.parts, blk_parts_of(s.nparts), blk_slot(0, 1, bn), parity, ctl);
+                       (const smx_part*)b.parts, blk_parts_of(s.nparts, s.rows), blk_slot(0, 1, bn), parity, ctl);
     return (int)hipGetLastError();
 }
 
@@ -797,7 +797,7 @@ bool block_args_ok(const smx_shape* shape, int k, int P, const void* blk, int64_
     if (!shape_ok(shape) || k < 0 || P < 1 || P > kBlkMax || !blk) return false;
     const smx_shape& s = *shape;
     if (s.row0 != 0 || s.rows != s.n || s.rows < 1 || s.m < 1) return false;
-    return blk_bytes >= blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts)).bytes;
+    return blk_bytes >= blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts, s.rows)).bytes;
 }
 
 // row-sharded blocks: any row block (a rank may own no rows), one f-row replica per rank
@@ -805,7 +805,7 @@ bool bshard_args_ok(const smx_shape* shape, int P, const void* blk, int64_t blk_
     if (!shape_ok(shape) || P < 1 || P > kBlkMax || !blk) return false;
     const smx_shape& s = *shape;
     if (s.rows < 0 || s.n < 1 || s.m < 1 || s.row0 < 0 || s.row0 + s.rows > s.n) return false;
-    return blk_bytes >= blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts)).bytes;
+    return blk_bytes >= blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts, s.rows)).bytes;
 }
 
 struct Graph {
@@ -1525,7 +1525,7 @@ int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout) {
     const int P = req > 0 ? req : block_pivots(*shape);
     if (P < 1 || !block_args_ok(shape, 0, P, shape, INT64_MAX)) return 0;
     if (pivots_inout) *pivots_inout = P;
-    return blk_layout(shape->rows + 1, shape->ld, blk_parts_of(shape->nparts)).bytes;
+    return blk_layout(shape->rows + 1, shape->ld, blk_parts_of(shape->nparts, shape->rows)).bytes;
 }
 
 int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
@@ -1614,7 +1614,7 @@ int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, i
 
 int64_t smx_bshard_bytes(const smx_shape* shape) {
     if (!bshard_args_ok(shape, 1, shape, INT64_MAX)) return 0;
-    return blk_layout(shape->rows + 1, shape->ld, blk_parts_of(shape->nparts)).bytes;
+    return blk_layout(shape->rows + 1, shape->ld, blk_parts_of(shape->nparts, shape->rows)).bytes;
 }
 
 int smx_bshard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,

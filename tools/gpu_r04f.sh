@@ -2,13 +2,13 @@
 # block path, planner traces old / P1 / P1+P3 on one box, per-pivot cost vs P, driver line
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r04e
+O=$R/gpurun_out/r04f
 mkdir -p $O
 cd $R
 
-timeout -k 10 600 python -u -m pytest tests/test_gpu_block_sharded.py tests/test_intzero.py tests/test_gpu_multi.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1
-rc=$?; echo "pytest rc=$rc" >> $O/pytest.txt; [ $rc -eq 0 ] || exit $rc
-for b in trace_planner_old trace_planner trace_planner_win; do
+
+
+for b in trace_planner_old trace_planner_p1 trace_planner_win; do
   timeout -k 10 120 tools/$b 16384 10 3 > $O/${b}_P10.jsonl || exit $?
   timeout -k 10 120 tools/$b 16384 20 2 > $O/${b}_P20.jsonl || exit $?
 done
