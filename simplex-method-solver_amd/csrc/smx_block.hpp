@@ -494,16 +494,19 @@ __device__ __forceinline__ void blk_rec_store(BlkRec R, smx_part* out) {
 
 // Every lane merges up to kBlkPartsMax / kWave records of a slot (loaded together: one round trip),
 // then the wave reduces them (the order of both merges is immaterial: total orders)
-__device__ __forceinline__ void blk_merge_records(const smx_part* __restrict__ slot, int G,
-                                                  int& nb, First& f, Cand& bb) {
-    constexpr int U = kBlkPartsMax / kWave;
+constexpr int kBlkRecU = kBlkPartsMax / kWave;   // records per lane of the merging wave
+__device__ __forceinline__ void blk_load_records(const smx_part* __restrict__ slot, int G,
+                                                 smx_part* p) {
     const int lane = threadIdx.x & (kWave - 1);
-    smx_part p[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < kBlkRecU; ++u) {
         const int k = lane + u * kWave;
         p[u] = k < G ? slot[k] : smx_part{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
     }
+}
+__device__ __forceinline__ void blk_reduce_records(const smx_part* p, int& nb, First& f,
+                                                   Cand& bb) {
+    constexpr int U = kBlkRecU;
     int n = SMX_NONE;
     First fi{SMX_NONE, 0.0};
     Cand b = cand_none();
@@ -517,6 +520,12 @@ __device__ __forceinline__ void blk_merge_records(const smx_part* __restrict__ s
     nb = wave_min_int_dpp(n);
     f = wave_first_dpp(fi);
     bb = wave_best_dpp(b);
+}
+__device__ __forceinline__ void blk_merge_records(const smx_part* __restrict__ slot, int G,
+                                                  int& nb, First& f, Cand& bb) {
+    smx_part p[kBlkRecU];
+    blk_load_records(slot, G, p);
+    blk_reduce_records(p, nb, f, bb);
 }
 
 // Records of a chain's first step, straight from T (workgroup b of nparts: local rows b*NT + tid
@@ -775,21 +784,20 @@ __device__ __forceinline__ bool blk_step_body(
     // f-row of T_{k+D} and the pivot rows pr_q at this thread's phase-2 columns (c0 = the column
     // the records of step D were built on, which is the entering column in phase 2; m; its slice
     // column; its first-round scan columns), and its first row's multipliers and cached columns.
-    // Nothing is pinned here (a pin would wait for the load); phase 1 discards them.
+    // Nothing is pinned here (a pin would wait for the load); phase 1 discards them.  (Tried
+    // and dropped: the first 32 columns of the thread's row staged in LDS by LDS-DMA for the
+    // row pass's column read -- row pass 2.51 vs 2.53 us, profiles/r04f/.)
+    // the merging wave's record loads go out first: the prefetches below queue behind them, and
+    // the wait for the records (vmcnt counts in issue order) does not include them
+    smx_part recs[kBlkRecU];
+    if (!SH && tid < kWave) blk_load_records(parts + (int64_t)blk_slot(D, P, bn) * G, G, recs);
     constexpr int NSC = NT >= 128 ? 1 : 128 / NT;   // first-round scan columns per thread
     constexpr int NJ = 2 + NSC;   // c or m (by lane parity), slice, scan columns
     int jj[NJ];
     double fv[NJ], pq[NJ][kBlkMax];
-    double pmq[kBlkMax], pxb = 0.0, pxc = 0.0;
+    double pmq[kBlkMax], pxb = 0.0, pxc = 0.0, pxa = 0.0;
+    bool pa_ok = false;   // pxa = T_k[i0][cf] issued by the phase-2 path
     const int i0 = b * NT + tid;
-    // The row pass reads T_k[i][cf] (and T_k[i][c] at step 0) for its rows: one 8-B load per row,
-    // each a different DRAM page.  The entering column is nearly always among the first columns
-    // (uniform LPs at 4096^2: median 6, 99.3 % below 32 over 300 pivots), so the first kWin
-    // columns of this thread's first row are staged in LDS at entry, beside the prefetches
-    // above, and the row pass reads its column from there when it falls inside.
-    constexpr int kWin = 32;
-    __shared__ double s_win[(SH || LAG) ? 1 : NT * kWin];
-    const bool use_win = !SH && !LAG && C >= kWin && b * NT < rows;
     const int c0 = SH || LAG ? 0 : hs->cfs[blk_slot(D, P, bn)];
     if constexpr (!SH && !LAG) {
         const int S = ((C + G - 1) / G + 1) & ~1;
@@ -803,21 +811,6 @@ __device__ __forceinline__ bool blk_step_body(
             fv[u] = fo_of(fr, sp, ld)[jc];
 #pragma unroll
             for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
-        }
-        if (use_win) {
-            // LDS-DMA: each wave loads the window of its own 64 rows (no VGPRs, no barrier; the
-            // row pass waits for vmcnt before its one read)
-            const int w = tid >> 6, lane = tid & (kWave - 1);
-            constexpr int LPR = kWin / 2;          // lanes per row (16 B each)
-            constexpr int RPI = kWave / LPR;       // rows per wave-instruction
-#pragma unroll
-            for (int k = 0; k < kWave / RPI; ++k) {
-                const int rw = w * kWave + k * RPI;
-                const int row = min(b * NT + rw + lane / LPR, rows - 1);
-                __builtin_amdgcn_global_load_lds(
-                    (const void*)(T + (int64_t)row * ld + (lane % LPR) * 2),
-                    (__attribute__((address_space(3))) void*)(s_win + rw * kWin), 16, 0, 0);
-            }
         }
         if (i0 < rows) {
             const double* mT0 = blk_mulT(mul, rows + 1);
@@ -850,7 +843,7 @@ __device__ __forceinline__ bool blk_step_body(
         int nb;
         First f;
         Cand bb;
-        blk_merge_records(parts + (int64_t)blk_slot(D, P, bn) * G, G, nb, f, bb);
+        blk_reduce_records(recs, nb, f, bb);
         Decision d;
         d.c = c;
         d.r = SMX_NONE;
@@ -990,17 +983,10 @@ __device__ __forceinline__ bool blk_step_body(
         e = blk_readlane(v[0], 0);
         fc = blk_readlane(fv[0], 0);
         SMX_BLK_STAMP(2);
-        // slice b of the pivot row and of the next f-row (columns beyond the first NT: as below)
-        if (jj[1] < s1) {
-            prD[jj[1]] = v[1];
-            fn[jj[1]] = blk_fnew(fv[1], v[1], jj[1], c, e, fc);
-        }
-        for (int j = s0 + tid + NT; j < s1; j += NT) {
-            const double vv = prv(j);
-            prD[j] = vv;
-            fn[j] = blk_fnew(fo[j], vv, j, c, e, fc);
-        }
-        SMX_BLK_STAMP(3);
+        // The next entering column first, then this thread's row-pass load of it, and only then
+        // this step's first stores: vmcnt counts loads and stores in one in-order queue, so a
+        // load issued after the slice stores could not be waited for without their write
+        // acknowledgements.
         // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
         int mine = SMX_NONE;
 #pragma unroll
@@ -1034,6 +1020,21 @@ __device__ __forceinline__ bool blk_step_body(
                     for (int q = 0; q < D; ++q) s_col[2][q] = pr[(int64_t)q * ld + cf];
             }
         }
+        if (cf != SMX_NONE && i0 < rows) {
+            pxa = T[(int64_t)i0 * ld + cf];   // the row pass's T_k[i0][cf], in flight from here
+            pa_ok = true;
+        }
+        // slice b of the pivot row and of the next f-row (columns beyond the first NT: as below)
+        if (jj[1] < s1) {
+            prD[jj[1]] = v[1];
+            fn[jj[1]] = blk_fnew(fv[1], v[1], jj[1], c, e, fc);
+        }
+        for (int j = s0 + tid + NT; j < s1; j += NT) {
+            const double vv = prv(j);
+            prD[j] = vv;
+            fn[j] = blk_fnew(fo[j], vv, j, c, e, fc);
+        }
+        SMX_BLK_STAMP(3);
         if (tid < 2) {   // lane 0 holds column c's operands, lane 1 column m's
             if (tid == 1) s_pm = v[0];
 #pragma unroll
@@ -1218,16 +1219,13 @@ __device__ __forceinline__ bool blk_step_body(
         const double* row = T + (int64_t)i * ld;
         double* mr = mul + (int64_t)i * kBlkMax;
         const bool pre = !SH && !LAG && i == i0;   // this thread's first row: prefetched at entry
-        const bool win = pre && use_win;
-        if (win) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS-DMA window landed
         const double xc = reuse_c ? (LAG ? colc[(int64_t)(D & 1) * rows + i]
                                          : (pre ? pxc : cca[(int64_t)(D & 1) * rows + i]))
-                                  : ((win && c < kWin) ? s_win[tid * kWin + c] : row[c]);
+                                  : row[c];
         const double xb = D > 0 ? (LAG ? colm[i]
                                        : (pre ? pxb : ccb[(int64_t)(D & 1) * rows + i]))
                                 : row[m];
-        const double xa = cf != SMX_NONE ? ((win && cf < kWin) ? s_win[tid * kWin + cf] : row[cf])
-                                         : 0.0;
+        const double xa = cf != SMX_NONE ? ((pre && pa_ok) ? pxa : row[cf]) : 0.0;
         if (LAG && D == 0) colm[i] = xb;
         if (LAG && cf != SMX_NONE) colc[(int64_t)(L & 1) * rows + i] = xa;
         double bv, a;

@@ -38,28 +38,36 @@ def main() -> None:
     T = lp.dense_tableau("uniform", 0, n, m)
     for world in (int(x) for x in a.ranks.split(",")):
         mt = MultiTableau(T, n, m, m, ["cuda:0"] * world, pivots=a.pivots)
-        mt.run(a.pivots)            # warm-up: prime, graphs of nothing, first kernels
+        mt.graph_chain = True
+        mt.run(a.pivots, graph=False)   # warm-up: prime, first kernels
         mt.sync_state()
-        host, wall = [], []
-        for _ in range(a.reps):
-            mt.upload(T)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            mt.run(a.k)
-            t1 = time.perf_counter()
-            st = mt.sync_state()
-            torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            assert int(st["npivots"]) == a.k, st
-            host.append((t1 - t0) / a.k * 1e6)
-            wall.append((t2 - t0) / a.k * 1e6)
-        dev = min(wall)
-        print(json.dumps({"size": a.size, "ranks": world, "exchange": mt.exchange,
-                          "pivots_per_sweep": a.pivots, "k": a.k,
-                          "host_us_per_pivot": round(min(host), 2),
-                          "device_us_per_pivot": round(dev, 2),
-                          "device_us_per_pivot_per_gpu": round(dev / world, 2),
-                          "host_bound_on_n_gpus": min(host) > dev / world}), flush=True)
+        logs = {}
+        for graph in (False, True):
+            host, wall = [], []
+            for rep in range(a.reps + (1 if graph else 0)):   # graph: the first run captures
+                mt.upload(T)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                mt.run(a.k, graph=graph)
+                t1 = time.perf_counter()
+                st = mt.sync_state()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                assert int(st["npivots"]) == a.k, st
+                if graph and rep == 0:
+                    continue
+                host.append((t1 - t0) / a.k * 1e6)
+                wall.append((t2 - t0) / a.k * 1e6)
+            logs[graph] = mt.read_log(0, a.k).tolist()
+            dev = min(wall)
+            print(json.dumps({"size": a.size, "ranks": world, "exchange": mt.exchange,
+                              "form": "graph" if graph else "eager",
+                              "pivots_per_sweep": a.pivots, "k": a.k,
+                              "host_us_per_pivot": round(min(host), 2),
+                              "device_us_per_pivot": round(dev, 2),
+                              "device_us_per_pivot_per_gpu": round(dev / world, 2),
+                              "host_bound_on_n_gpus": min(host) > dev / world}), flush=True)
+        assert logs[False] == logs[True], "graph and eager trajectories differ"
         mt.close()
         del mt
         torch.cuda.empty_cache()
