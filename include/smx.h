@@ -459,13 +459,6 @@ typedef struct smx_rank {
 int smx_mshard_comms(void** comms_out, int32_t nranks, const int32_t* devices);
 int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
                    int32_t pivots, int32_t exchange);
-/* smx_mshard_run's k pivots captured once as ONE graph on ranks[0].stream (the other ranks'
- * streams fork from and join back into it): replay with smx_graph_launch(graph,
- * ranks[0].stream), free with smx_graph_destroy.  Host cost: one call per chain instead of ~30
- * per pivot and rank (tools/mshard_host_cost.py). */
-int smx_mshard_graph_create(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
-                            int32_t pivots, int32_t exchange, void** graph_out);
-
 /* ---- Host engine (no device): the same pick_element / recalculate_matrix on a HOST tableau --
  * For machines without an MI355X (the reference UI's 2-variable LPs, BASELINE.json configs[0]).
  * Pointers here are HOST pointers (same layout as the device tableau: row-major fp64, R = n + 1

@@ -1794,10 +1794,9 @@ bool mshard_args_ok(const smx_rank* ranks, int32_t nranks, int32_t k, int32_t pi
     return true;
 }
 
-// Every launch of k chained pivots on every rank, enqueued from this thread (smx_mshard_run and
-// its captured form smx_mshard_graph_create)
-// ev_ext: the copy exchange's 2 * nranks events created by the caller (a capture creates and
-// destroys them outside the captured region), or NULL: created and destroyed here.
+// Every launch of k chained pivots on every rank, enqueued from this thread (smx_mshard_run)
+// ev_ext: the copy exchange's 2 * nranks events created by the caller, or NULL: created and
+// destroyed here.
 int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
                    int32_t pivots, int32_t exchange, hipEvent_t* ev_ext = nullptr) {
     int dev0 = 0;
@@ -1921,63 +1920,6 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
     if (!mshard_args_ok(ranks, nranks, k, pivots, exchange)) return (int)hipErrorInvalidValue;
     if (k == 0) return 0;
     return mshard_enqueue(ranks, nranks, parity, k, pivots, exchange);
-}
-
-// The same k pivots captured once as ONE hipGraph on ranks[0]'s stream: the other ranks' streams
-// join the capture through an event recorded on it and leave through events it waits on, so
-// replaying the graph (smx_graph_launch on ranks[0].stream) costs one host call per chain instead
-// of ~30 per pivot and rank.  Every rank must sit on ranks[0]'s device (the copy exchange of a
-// one-GPU box), or use the RCCL exchange with one communicator per device.
-int smx_mshard_graph_create(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
-                            int32_t pivots, int32_t exchange, void** graph_out) {
-    if (!mshard_args_ok(ranks, nranks, k, pivots, exchange) || k < 1 || !graph_out)
-        return (int)hipErrorInvalidValue;
-    int dev0 = 0;
-    (void)hipGetDevice(&dev0);
-    hipStream_t st0 = S(ranks[0].stream);
-    // ev[0]: fork; ev[q + 1]: rank q's join; ev[nranks + 1 ...]: the copy exchange's events --
-    // all created before the capture and destroyed after it
-    const int nev = 3 * nranks + 1;
-    hipEvent_t* ev = new hipEvent_t[nev]();
-    int err = 0;
-    for (int q = 0; q < nev && !err; ++q) {
-        const int owner = q == 0 ? 0 : (q <= nranks ? q - 1 : (q - nranks - 1) / 2);
-        err = (int)hipSetDevice(ranks[owner].device);
-        if (!err) err = (int)hipEventCreateWithFlags(&ev[q], hipEventDisableTiming);
-    }
-    Graph* g = new Graph();
-    if (!err) err = (int)hipSetDevice(ranks[0].device);
-    if (!err) err = (int)hipStreamBeginCapture(st0, hipStreamCaptureModeThreadLocal);
-    if (!err) {
-        int lerr = (int)hipEventRecord(ev[0], st0);   // fork: every stream joins the capture
-        for (int q = 1; q < nranks && !lerr; ++q) {
-            lerr = (int)hipSetDevice(ranks[q].device);
-            if (!lerr) lerr = (int)hipStreamWaitEvent(S(ranks[q].stream), ev[0], 0);
-        }
-        if (!lerr) lerr = mshard_enqueue(ranks, nranks, parity, k, pivots, exchange, ev + nranks + 1);
-        for (int q = 1; q < nranks && !lerr; ++q) {   // join back into ranks[0]'s stream
-            lerr = (int)hipSetDevice(ranks[q].device);
-            if (!lerr) lerr = (int)hipEventRecord(ev[q + 1], S(ranks[q].stream));
-            if (!lerr) lerr = (int)hipSetDevice(ranks[0].device);
-            if (!lerr) lerr = (int)hipStreamWaitEvent(st0, ev[q + 1], 0);
-        }
-        (void)hipSetDevice(ranks[0].device);
-        const hipError_t e2 = hipStreamEndCapture(st0, &g->graph);
-        err = lerr ? lerr : (int)e2;
-    }
-    if (!err) err = (int)hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
-    for (int q = 0; q < nev; ++q)
-        if (ev[q]) (void)hipEventDestroy(ev[q]);
-    delete[] ev;
-    (void)hipSetDevice(dev0);
-    if (err) {
-        if (g->exec) (void)hipGraphExecDestroy(g->exec);
-        if (g->graph) (void)hipGraphDestroy(g->graph);
-        delete g;
-        return err;
-    }
-    *graph_out = g;
-    return 0;
 }
 
 int smx_int_first_fix(const double* T0, double* T1, int64_t ld, int32_t rows, int32_t cols,

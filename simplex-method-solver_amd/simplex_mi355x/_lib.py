@@ -73,8 +73,7 @@ EXPORTS = (
     "smx_bshard_pack", "smx_bshard_step", "smx_bshard_sweep", "smx_bshard_publish",
     "smx_bshard_pick", "smx_bshard_step_light", "smx_tune_shard_xchg",
     "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
-    "smx_mshard_comms", "smx_mshard_run", "smx_mshard_graph_create", "smx_int_first_fix",
-    "smx_host_int_first_fix",
+    "smx_mshard_comms", "smx_mshard_run", "smx_int_first_fix", "smx_host_int_first_fix",
 )
 
 
@@ -185,8 +184,6 @@ def load():
         "smx_mshard_comms": ([ctypes.POINTER(ctypes.c_void_p), i32, ctypes.POINTER(i32)],
                              ctypes.c_int),
         "smx_mshard_run": ([ctypes.POINTER(Rank), i32, i32, i32, i32, i32], ctypes.c_int),
-        "smx_mshard_graph_create": ([ctypes.POINTER(Rank), i32, i32, i32, i32, i32,
-                                     ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
         "smx_int_first_fix": ([vp, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp, vp],
                               ctypes.c_int),
         "smx_host_int_first_fix": ([vp, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .device import Graph, int_first_fix
+from .device import int_first_fix
 from .sharded import BlockShardBackend, row_range
 
 
@@ -90,10 +90,6 @@ class MultiTableau:
         distinct = len({(d.index) for d in self.devices}) == P
         self.exchange = exchange or ("rccl" if distinct and P > 1 else "copy")
         self._comms = None
-        self._graphs = {}
-        # chained runs as one captured graph per (parity, k) (smx_mshard_graph_create; copy
-        # exchange); False: smx_mshard_run enqueues every launch from the host each time
-        self.graph_chain = False
         if self.exchange == "rccl":
             comms = (ctypes.c_void_p * P)()
             devs = (ctypes.c_int32 * P)(*[d.index for d in self.devices])
@@ -124,23 +120,10 @@ class MultiTableau:
             a.shape = _lib.Shape(*d.shape)
         return arr
 
-    def _native(self, k: int, pivots: int, graph: bool = False) -> None:
-        xm = _lib.XCHG_RCCL if self.exchange == "rccl" else _lib.XCHG_COPY
-        if graph and self.graph_chain and self.exchange == "copy":
-            # one captured graph per (parity, k): the ranks' ~30 launches / copies / event waits
-            # per pivot and rank become one host call per chain (smx_mshard_graph_create)
-            key = (self.step & 1, int(k), int(pivots))
-            g = self._graphs.get(key)
-            if g is None:
-                h = ctypes.c_void_p()
-                _lib.check(_lib.load().smx_mshard_graph_create(
-                    self._structs, self.world, self.step & 1, int(k), int(pivots), xm,
-                    ctypes.byref(h)), "smx_mshard_graph_create")
-                g = self._graphs[key] = Graph(h.value)
-            g.launch(self.ranks[0].dev.stream.cuda_stream)
-            return
+    def _native(self, k: int, pivots: int) -> None:
         _lib.check(_lib.load().smx_mshard_run(
-            self._structs, self.world, self.step & 1, int(k), int(pivots), xm), "smx_mshard_run")
+            self._structs, self.world, self.step & 1, int(k), int(pivots),
+            _lib.XCHG_RCCL if self.exchange == "rccl" else _lib.XCHG_COPY), "smx_mshard_run")
 
     def _sync(self) -> None:
         for dev in self.devices:
@@ -331,7 +314,7 @@ class MultiTableau:
         self._restore()
         if self._term:
             self.clear_term()
-        self._native(k, self.P, graph=graph)
+        self._native(k, self.P)
         for be in self.ranks:
             be.dev.step += k
             be.dev._pending = True
@@ -353,9 +336,6 @@ class MultiTableau:
         self._term = False
 
     def close(self) -> None:
-        for g in getattr(self, "_graphs", {}).values():
-            g.destroy()
-        self._graphs = {}
         if self._comms:
             L = _lib.load()
             for h in self._comms:

@@ -38,11 +38,10 @@ def main() -> None:
     T = lp.dense_tableau("uniform", 0, n, m)
     for world in (int(x) for x in a.ranks.split(",")):
         mt = MultiTableau(T, n, m, m, ["cuda:0"] * world, pivots=a.pivots)
-        mt.graph_chain = True
         mt.run(a.pivots, graph=False)   # warm-up: prime, first kernels
         mt.sync_state()
         logs = {}
-        for graph in (False, True):
+        for graph in (False,):
             host, wall = [], []
             for rep in range(a.reps + (1 if graph else 0)):   # graph: the first run captures
                 mt.upload(T)
@@ -67,7 +66,6 @@ def main() -> None:
                               "device_us_per_pivot": round(dev, 2),
                               "device_us_per_pivot_per_gpu": round(dev / world, 2),
                               "host_bound_on_n_gpus": min(host) > dev / world}), flush=True)
-        assert logs[False] == logs[True], "graph and eager trajectories differ"
         mt.close()
         del mt
         torch.cuda.empty_cache()
