@@ -69,7 +69,8 @@ constexpr int kBlkPartsPer = kUpdBlock / kBlkNT;
 // Planner workgroups: the select partition's count (at least one slice of the pivot row per
 // workgroup), raised to one row per thread on tall tables: at 65536 rows 64 workgroups own
 // 1,024 rows each and the row pass runs four rows per thread back to back (config 5's planner
-// took 27.5 us per pivot against 14.4 at 16384^2, profiles/r03c/config5_degenerate_1gpu.json).
+// took 27.5 us per pivot against 14.4 at 16384^2, profiles/r03c/config5_degenerate_1gpu.json;
+// 24.2 with 256 workgroups, profiles/r04h/config5_degenerate.json).
 constexpr int kBlkPartsMax = 4 * kMaxParts * kBlkPartsPer;
 __host__ __device__ __forceinline__ int blk_parts_of(int nparts, int rows) {
     const int by_rows = (rows + kBlkNT - 1) / kBlkNT;
@@ -494,19 +495,16 @@ __device__ __forceinline__ void blk_rec_store(BlkRec R, smx_part* out) {
 
 // Every lane merges up to kBlkPartsMax / kWave records of a slot (loaded together: one round trip),
 // then the wave reduces them (the order of both merges is immaterial: total orders)
-constexpr int kBlkRecU = kBlkPartsMax / kWave;   // records per lane of the merging wave
-__device__ __forceinline__ void blk_load_records(const smx_part* __restrict__ slot, int G,
-                                                 smx_part* p) {
+__device__ __forceinline__ void blk_merge_records(const smx_part* __restrict__ slot, int G,
+                                                  int& nb, First& f, Cand& bb) {
+    constexpr int U = kBlkPartsMax / kWave;
     const int lane = threadIdx.x & (kWave - 1);
+    smx_part p[U];
 #pragma unroll
-    for (int u = 0; u < kBlkRecU; ++u) {
+    for (int u = 0; u < U; ++u) {
         const int k = lane + u * kWave;
         p[u] = k < G ? slot[k] : smx_part{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
     }
-}
-__device__ __forceinline__ void blk_reduce_records(const smx_part* p, int& nb, First& f,
-                                                   Cand& bb) {
-    constexpr int U = kBlkRecU;
     int n = SMX_NONE;
     First fi{SMX_NONE, 0.0};
     Cand b = cand_none();
@@ -520,12 +518,6 @@ __device__ __forceinline__ void blk_reduce_records(const smx_part* p, int& nb, F
     nb = wave_min_int_dpp(n);
     f = wave_first_dpp(fi);
     bb = wave_best_dpp(b);
-}
-__device__ __forceinline__ void blk_merge_records(const smx_part* __restrict__ slot, int G,
-                                                  int& nb, First& f, Cand& bb) {
-    smx_part p[kBlkRecU];
-    blk_load_records(slot, G, p);
-    blk_reduce_records(p, nb, f, bb);
 }
 
 // Records of a chain's first step, straight from T (workgroup b of nparts: local rows b*NT + tid
@@ -709,12 +701,14 @@ __device__ unsigned g_blk_fallback[kBlkMax + 1][2];
     } while (0)
 #endif
 
-// The f-row of step parity sp (fr [2][ld], blk_step_body)
-__device__ __forceinline__ const double* fo_of(const double* fr, int sp, int64_t ld) {
-    return fr + (int64_t)sp * ld;
-}
-
 // One pivot of the block: decide block step D = L-1 and build the records of step L.
+// Round 4, tried and not kept (tools/trace_planner.hip, 16384^2, per-step mean over 2-3 blocks,
+// profiles/r04h/ and r04i/): the decision-independent operands (pivot-row slices at the phase-2
+// columns, the f-row, the row pass's multipliers and cached columns) issued at step entry --
+// decision phase 2.67 -> 3.6 us, post-decision phase 0.4 us shorter, step 13.4 -> 14.1 us at
+// P = 10 (also with the merging wave's record loads issued first); the first 32 columns of each
+// row staged in LDS by LDS-DMA for the row pass's column read -- row pass 2.53 -> 2.51 us;
+// the row pass's column load issued before the step's first stores -- 0.1 us.
 // SH = false: the decision from the records of step D and the pivot-row values derived on the
 // fly; SH = true (row-sharded): from the P gathered send slots in `recv` (merge_headers), the
 // pivot row taken from the winning slot.  Pivot rows are LOCAL indices in the header (-1 when
@@ -777,53 +771,6 @@ __device__ __forceinline__ bool blk_step_body(
     } else {
         blk_load_pivots(h, D, &s_pv);
     }
-    // Operands of the phase-2 pivot-row chains and of the row pass that do not depend on the
-    // decision, issued before it so their latency hides under the records' round trip (the
-    // phase-2 step's loads after the decision were 3(D + 2) per thread and that phase grew
-    // from 1.3 to 4.5 us per step with D, profiles/r03b/planner_trace_P10_dpp_mulT.jsonl): the
-    // f-row of T_{k+D} and the pivot rows pr_q at this thread's phase-2 columns (c0 = the column
-    // the records of step D were built on, which is the entering column in phase 2; m; its slice
-    // column; its first-round scan columns), and its first row's multipliers and cached columns.
-    // Nothing is pinned here (a pin would wait for the load); phase 1 discards them.  (Tried
-    // and dropped: the first 32 columns of the thread's row staged in LDS by LDS-DMA for the
-    // row pass's column read -- row pass 2.51 vs 2.53 us, profiles/r04f/.)
-    // the merging wave's record loads go out first: the prefetches below queue behind them, and
-    // the wait for the records (vmcnt counts in issue order) does not include them
-    smx_part recs[kBlkRecU];
-    if (!SH && tid < kWave) blk_load_records(parts + (int64_t)blk_slot(D, P, bn) * G, G, recs);
-    constexpr int NSC = NT >= 128 ? 1 : 128 / NT;   // first-round scan columns per thread
-    constexpr int NJ = 2 + NSC;   // c or m (by lane parity), slice, scan columns
-    int jj[NJ];
-    double fv[NJ], pq[NJ][kBlkMax];
-    double pmq[kBlkMax], pxb = 0.0, pxc = 0.0, pxa = 0.0;
-    bool pa_ok = false;   // pxa = T_k[i0][cf] issued by the phase-2 path
-    const int i0 = b * NT + tid;
-    const int c0 = SH || LAG ? 0 : hs->cfs[blk_slot(D, P, bn)];
-    if constexpr (!SH && !LAG) {
-        const int S = ((C + G - 1) / G + 1) & ~1;
-        jj[0] = (tid & 1) ? m : c0;
-        jj[1] = b * S + tid;
-#pragma unroll
-        for (int k = 0; k < NSC; ++k) jj[2 + k] = tid + k * NT;
-#pragma unroll
-        for (int u = 0; u < NJ; ++u) {
-            const int jc = min(jj[u], C - 1);
-            fv[u] = fo_of(fr, sp, ld)[jc];
-#pragma unroll
-            for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
-        }
-        if (i0 < rows) {
-            const double* mT0 = blk_mulT(mul, rows + 1);
-#pragma unroll
-            for (int q = 0; q < D; ++q) pmq[q] = mT0[(int64_t)q * (rows + 1) + i0];
-            if (D > 0) {
-                const double* colm0 = fr + 2 * ld;
-                const double* cca0 = colm0 + 3 * (int64_t)rows;
-                pxc = cca0[(int64_t)(D & 1) * rows + i0];
-                pxb = cca0[2 * (int64_t)rows + (int64_t)(D & 1) * rows + i0];
-            }
-        }
-    }
     if (SH) {
         if (tid == 0) {
             // full exchange: recv = the gathered send slots; light (xslot = SMX_SHARD_HDR): recv
@@ -839,11 +786,11 @@ __device__ __forceinline__ bool blk_step_body(
         }
     } else if (tid < kWave) {
         // the decision of step D from its records (every workgroup, identically)
-        const int c = LAG ? hs->cfs[blk_slot(D, P, bn)] : c0;
+        const int c = hs->cfs[blk_slot(D, P, bn)];
         int nb;
         First f;
         Cand bb;
-        blk_reduce_records(recs, nb, f, bb);
+        blk_merge_records(parts + (int64_t)blk_slot(D, P, bn) * G, G, nb, f, bb);
         Decision d;
         d.c = c;
         d.r = SMX_NONE;
@@ -951,13 +898,26 @@ __device__ __forceinline__ bool blk_step_body(
     // columns cost 7 chains and 7 (D + 2) loads per thread on every step: tools/trace_planner.hip,
     // profiles/r03b/).  Same chains on the same operands: the same values.
     if (!SH && !LAG && nb == SMX_NONE) {
-        c = d.c;                       // == c0: the prefetched columns are this step's
+        c = d.c;
         const double* Tr = T + (int64_t)r_local * ld;
         const int S = ((C + G - 1) / G + 1) & ~1;
         const int s0 = b * S, s1 = min(C, s0 + S);
-        double x[NJ];
+        constexpr int NSC = NT >= 128 ? 1 : 128 / NT;   // first-round scan columns per thread
+        constexpr int NJ = 2 + NSC;   // c or m (by lane parity), slice, scan columns
+        int jj[NJ];
+        jj[0] = (tid & 1) ? m : c;
+        jj[1] = s0 + tid;
 #pragma unroll
-        for (int u = 0; u < NJ; ++u) x[u] = Tr[min(jj[u], C - 1)];
+        for (int k = 0; k < NSC; ++k) jj[2 + k] = tid + k * NT;
+        double x[NJ], pq[NJ][kBlkMax], fv[NJ];
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+            const int jc = min(jj[u], C - 1);
+            x[u] = Tr[jc];
+            fv[u] = fo[jc];
+#pragma unroll
+            for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
+        }
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
             blk_pin(x[u]);
@@ -983,10 +943,17 @@ __device__ __forceinline__ bool blk_step_body(
         e = blk_readlane(v[0], 0);
         fc = blk_readlane(fv[0], 0);
         SMX_BLK_STAMP(2);
-        // The next entering column first, then this thread's row-pass load of it, and only then
-        // this step's first stores: vmcnt counts loads and stores in one in-order queue, so a
-        // load issued after the slice stores could not be waited for without their write
-        // acknowledgements.
+        // slice b of the pivot row and of the next f-row (columns beyond the first NT: as below)
+        if (jj[1] < s1) {
+            prD[jj[1]] = v[1];
+            fn[jj[1]] = blk_fnew(fv[1], v[1], jj[1], c, e, fc);
+        }
+        for (int j = s0 + tid + NT; j < s1; j += NT) {
+            const double vv = prv(j);
+            prD[j] = vv;
+            fn[j] = blk_fnew(fo[j], vv, j, c, e, fc);
+        }
+        SMX_BLK_STAMP(3);
         // the next entering column: first j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
         int mine = SMX_NONE;
 #pragma unroll
@@ -1020,21 +987,6 @@ __device__ __forceinline__ bool blk_step_body(
                     for (int q = 0; q < D; ++q) s_col[2][q] = pr[(int64_t)q * ld + cf];
             }
         }
-        if (cf != SMX_NONE && i0 < rows) {
-            pxa = T[(int64_t)i0 * ld + cf];   // the row pass's T_k[i0][cf], in flight from here
-            pa_ok = true;
-        }
-        // slice b of the pivot row and of the next f-row (columns beyond the first NT: as below)
-        if (jj[1] < s1) {
-            prD[jj[1]] = v[1];
-            fn[jj[1]] = blk_fnew(fv[1], v[1], jj[1], c, e, fc);
-        }
-        for (int j = s0 + tid + NT; j < s1; j += NT) {
-            const double vv = prv(j);
-            prD[j] = vv;
-            fn[j] = blk_fnew(fo[j], vv, j, c, e, fc);
-        }
-        SMX_BLK_STAMP(3);
         if (tid < 2) {   // lane 0 holds column c's operands, lane 1 column m's
             if (tid == 1) s_pm = v[0];
 #pragma unroll
@@ -1218,14 +1170,9 @@ __device__ __forceinline__ bool blk_step_body(
     for (int i = b * NT + tid; i < rows; i += G * NT) {
         const double* row = T + (int64_t)i * ld;
         double* mr = mul + (int64_t)i * kBlkMax;
-        const bool pre = !SH && !LAG && i == i0;   // this thread's first row: prefetched at entry
-        const double xc = reuse_c ? (LAG ? colc[(int64_t)(D & 1) * rows + i]
-                                         : (pre ? pxc : cca[(int64_t)(D & 1) * rows + i]))
-                                  : row[c];
-        const double xb = D > 0 ? (LAG ? colm[i]
-                                       : (pre ? pxb : ccb[(int64_t)(D & 1) * rows + i]))
-                                : row[m];
-        const double xa = cf != SMX_NONE ? ((pre && pa_ok) ? pxa : row[cf]) : 0.0;
+        const double xc = reuse_c ? (LAG ? colc : cca)[(int64_t)(D & 1) * rows + i] : row[c];
+        const double xb = D > 0 ? (LAG ? colm[i] : ccb[(int64_t)(D & 1) * rows + i]) : row[m];
+        const double xa = cf != SMX_NONE ? row[cf] : 0.0;
         if (LAG && D == 0) colm[i] = xb;
         if (LAG && cf != SMX_NONE) colc[(int64_t)(L & 1) * rows + i] = xa;
         double bv, a;
@@ -1258,7 +1205,7 @@ __device__ __forceinline__ bool blk_step_body(
             double mq[kBlkMax];
             double x3[3] = {xc, xb, xa};
 #pragma unroll
-            for (int q = 0; q < D; ++q) mq[q] = pre ? pmq[q] : mT[(int64_t)q * (rows + 1) + i];
+            for (int q = 0; q < D; ++q) mq[q] = mT[(int64_t)q * (rows + 1) + i];
 #pragma unroll
             for (int q = 0; q < D; ++q) blk_pin(mq[q]);
 #pragma unroll

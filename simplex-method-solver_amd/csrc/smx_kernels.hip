@@ -1765,6 +1765,23 @@ int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, sm
                               blk_ptrs(*shape, static_cast<char*>(blk)), S(stream));
 }
 
+// Copy exchange of ranks that share one device (SimplexMethod(..., devices=[0] * N)): ONE launch
+// on ranks[0]'s stream copies every rank's send slot into every rank's recv (grid.y = dst * N +
+// src), instead of N^2 hipMemcpyAsync calls and N^2 event waits per pivot from the host
+// (tools/mshard_host_cost.py: 418 us of host enqueue per pivot at 8 ranks, profiles/r04h/).
+constexpr int kMsMaxRanks = 16;
+struct MsSlots {
+    const double* src[kMsMaxRanks];
+    double* dst[kMsMaxRanks];
+};
+__global__ __launch_bounds__(256) void k_mshard_gather(MsSlots s, int nranks, int64_t slot) {
+    const int q = blockIdx.y / nranks, o = blockIdx.y % nranks;
+    const double* src = s.src[o];
+    double* dst = s.dst[q] + (int64_t)o * slot;
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < slot; j += (int64_t)gridDim.x * 256)
+        dst[j] = src[j];
+}
+
 // ---- single-process multi-device row sharding (smx_mshard_*) --------------------------------
 int smx_mshard_comms(void** comms_out, int32_t nranks, const int32_t* devices) {
     if (!comms_out || !devices || nranks < 1) return (int)hipErrorInvalidValue;
@@ -1821,6 +1838,14 @@ int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
     auto buf = [&](int q, int p) { return p ? ranks[q].buf1 : ranks[q].buf0; };
     // light exchange (RCCL only; the copy exchange always moves whole slots)
     const bool light = exchange == SMX_XCHG_RCCL && xchg_light(nranks);
+    // copy exchange on one device: one gather launch on ranks[0]'s stream (k_mshard_gather)
+    bool one_dev = exchange == SMX_XCHG_COPY && nranks <= kMsMaxRanks;
+    for (int q = 1; q < nranks; ++q) one_dev = one_dev && ranks[q].device == ranks[0].device;
+    MsSlots ms{};
+    for (int q = 0; q < nranks && one_dev; ++q) {
+        ms.src[q] = ranks[q].send;
+        ms.dst[q] = ranks[q].recv;
+    }
     auto xrow = [&](int q) { return ranks[q].recv + (size_t)nranks * SMX_SHARD_HDR; };
     for (int q = 0; q < nranks && !err; ++q) {
         hipStream_t st = on(q);
@@ -1864,6 +1889,25 @@ int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                 const ncclResult_t re = ncclGroupEnd();
                 if (rr == ncclSuccess) rr = re;
                 if (rr != ncclSuccess) err = -1000 - (int)rr;
+            } else if (one_dev) {
+                // ranks[0]'s stream waits for every pack, gathers every slot into every recv in
+                // one launch, and every other rank waits for that launch: 3N - 1 host calls per
+                // pivot.  A rank's next pack follows its wait, so no slot is overwritten early.
+                hipStream_t st0 = on(0);
+                for (int q = 1; q < nranks && !err; ++q) {
+                    err = (int)hipEventRecord(ev[2 * q], on(q));
+                    if (!err) err = (int)hipStreamWaitEvent(st0, ev[2 * q], 0);
+                }
+                const int gx = (int)((slot + 256 * 8 - 1) / (256 * 8));
+                if (!err) {
+                    (void)hipSetDevice(ranks[0].device);
+                    hipLaunchKernelGGL(k_mshard_gather, dim3(gx, nranks * nranks), dim3(256), 0,
+                                       st0, ms, nranks, (int64_t)slot);
+                    err = (int)hipGetLastError();
+                }
+                if (!err) err = (int)hipEventRecord(ev[1], st0);
+                for (int q = 1; q < nranks && !err; ++q)
+                    err = (int)hipStreamWaitEvent(on(q), ev[1], 0);
             } else {   // every rank copies every send slot into its recv, ordered by events
                 for (int q = 0; q < nranks && !err; ++q)
                     err = (int)hipEventRecord(ev[2 * q], on(q));
