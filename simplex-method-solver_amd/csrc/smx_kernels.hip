@@ -318,8 +318,11 @@ constexpr int64_t kResLdsMin = 82 * 1024;               // > half a CU's LDS: on
 
 struct ResPlan {
     int G, rpw, ept;
-    int64_t lds, rec_bytes, row_off, bytes;
+    int64_t lds, rec_bytes, row_off, pc_off, bytes;
 };
+// 1: the overlapped loop (k_resident<true>: the bulk update hidden under the next hand-off's
+// poll); 0: the round-3 loop (smx_tune_resident_overlap)
+int g_resident_ovl = 1;
 
 bool resident_plan(const smx_shape& s, ResPlan* p) {
     if (g_resident < 0) return false;
@@ -346,7 +349,8 @@ bool resident_plan(const smx_shape& s, ResPlan* p) {
     p->lds = lds < kResLdsMin ? kResLdsMin : lds;
     p->rec_bytes = (int64_t)2 * G * kResRecWords * 8;
     p->row_off = (p->rec_bytes + 255) / 256 * 256;
-    p->bytes = p->row_off + (int64_t)2 * G * 2 * (2 * s.ld) * 8;   // rows as tagged granules
+    p->pc_off = p->row_off + (int64_t)2 * G * 2 * (2 * s.ld) * 8;  // rows as tagged granules
+    p->bytes = p->pc_off + (int64_t)2 * G * 2 * 2 * 8;              // their pivot-column entries
     return true;
 }
 
@@ -355,17 +359,20 @@ int launch_resident_kernel(double* buf0, double* buf1, const smx_shape& s, const
                            int32_t* log, double* xhist, int64_t log_cap, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_resident,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)kResLdsMax);
-        if (e != hipSuccess) return (int)e;
+        for (const void* f : {(const void*)k_resident<true>, (const void*)k_resident<false>}) {
+            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)kResLdsMax);
+            if (e != hipSuccess) return (int)e;
+        }
         attr = true;
     }
-    hipLaunchKernelGGL(k_resident, dim3(p.G), dim3(kResBlock), (size_t)p.lds, st, buf0, buf1,
+    hipLaunchKernelGGL(g_resident_ovl ? k_resident<true> : k_resident<false>, dim3(p.G),
+                       dim3(kResBlock), (size_t)p.lds, st, buf0, buf1,
                        s.ld, s.n, s.m, s.flen, fscan_of(s), parity, k, p.rpw, ctl, log, xhist,
                        log_cap, reinterpret_cast<uint64_t*>(xch),
                        reinterpret_cast<uint64_t*>(xch + p.row_off), s.ld, epoch,
-                       g_resident_trace, g_resident_trace_from);
+                       g_resident_trace, g_resident_trace_from,
+                       reinterpret_cast<uint64_t*>(xch + p.pc_off));
     return (int)hipGetLastError();
 }
 
@@ -1428,6 +1435,12 @@ int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_
                                      stream);
     if (ev_after) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_after), S(stream));
     return err;
+}
+
+int smx_tune_resident_overlap(int32_t on) {
+    const int prev = g_resident_ovl;
+    if (on >= 0) g_resident_ovl = on ? 1 : 0;
+    return prev;
 }
 
 int smx_tune_resident(int32_t workgroups) {

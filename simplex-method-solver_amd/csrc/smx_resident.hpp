@@ -135,12 +135,21 @@ struct ResDecision {
     int cf;                            // first negative f-row column (ctl->negf)
 };
 
+// OVL (round 4, the default): the bulk of step s's Jordan step overlaps step s+1's hand-off.
+// After staging pivot row s, only the f-row and the "-b" column are updated (E1); the records
+// of step s+1 read every other value they need -- the entering column, the phase-1 row -- as
+// T_{s+1} = upd_s(T_s) on the fly, the candidate rows are published as T_s values plus their
+// pivot-column entry (xpc), and the rest of the table (E2) is updated by the twelve non-polling
+// waves WHILE the four polling waves wait for the other workgroups' records.  The receiver of a
+// row applies the same upd_s to it when staging it.  Same operations on the same operands in
+// the same order: the same bits.
+template <bool OVL>
 __global__ __launch_bounds__(kResBlock) void k_resident(
     double* __restrict__ buf0, double* __restrict__ buf1, int64_t ld, int n, int m, int flen,
     int fscan, int parity, int k, int rpw, smx_ctl* __restrict__ ctl, int32_t* __restrict__ log,
     double* __restrict__ xhist, int64_t log_cap, uint64_t* __restrict__ xrec,
     uint64_t* __restrict__ xrow, int64_t ldx, uint32_t epoch, uint64_t* __restrict__ trace,
-    int trace_from) {
+    int trace_from, uint64_t* __restrict__ xpc) {
     extern __shared__ double s_T[];   // (rpw + 1) rows of ldl, then s_prow[C], then s_pc[rpw + 1]
     __shared__ uint32_t s_rec[kResPollers][kResRecWords];
     __shared__ ResWave s_wred[kResPollers / kWave];
@@ -208,6 +217,23 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
     ResDecision d;
     int last_r = SMX_NONE, last_c = SMX_NONE;
     double last_e = 0.0;
+    // OVL: step s-1's pivot while its bulk update is still pending (lag): s_prow / s_pc hold its
+    // pivot row and column, every value outside the f-row and the "-b" column is T_{s-1}
+    bool lag = false;
+    int rp_local = -1, cp = SMX_NONE, rp = SMX_NONE;
+    double ep = 1.0;
+    FastDiv fdp{1.0, 1.0, true};
+    auto updp = [&](bool isr, bool isc, double x, double pr, double pc) -> double {
+        const double t = x * ep - pr * pc;
+        const double num = isr ? (isc ? 1.0 : -x) : (isc ? x : t);
+        return fd_div(num, fdp);
+    };
+    // T_s[l][j] of an own row (OVL): the LDS value, or upd_{s-1} of it outside the "-b" column
+    auto curv = [&](int l, int j) -> double {
+        const double x = s_T[l * ldl + j];
+        if (!OVL || !lag || j == m) return x;
+        return updp(l == rp_local, j == cp, x, s_prow[j], s_pc[l]);
+    };
     for (;; ++s) {
         const uint32_t want = (epoch << 20) | (uint32_t)(s + 1);
         const uint64_t tag = (uint64_t)want << 32;
@@ -241,7 +267,7 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                 const int il = lb - row0;
                 for (int jb = 0; jb < m; jb += kWave) {
                     const int j = jb + lane;
-                    const uint64_t mk = __ballot(j < m && s_T[il * ldl + j] > 0.0);
+                    const uint64_t mk = __ballot(j < m && curv(il, j) > 0.0);
                     if (mk) {
                         p1 = jb + __ffsll((long long)mk) - 1;
                         break;
@@ -253,7 +279,7 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                 int c1 = SMX_NONE, c2 = SMX_NONE;
                 for (int ib = 0; ib < nl; ib += kWave) {
                     const int i = ib + lane;
-                    const double a = (i < nl) ? s_T[i * ldl + cf] : 0.0;
+                    const double a = (i < nl) ? curv(i, cf) : 0.0;
                     const bool cand = (i < nl) && a != 0.0;
                     const double v = cand ? s_T[i * ldl + m] / a : 0.0;
                     const uint64_t mf = __ballot(cand);
@@ -315,6 +341,15 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                 };
                 if (rb >= 0) put(dst + ldg, rb - row0);
                 if (ra >= 0) put(dst, ra - row0);
+                if (OVL && lag && lane < 2) {   // the rows' step s-1 pivot-column entries
+                    const int rr = lane ? rb : ra;   // lane 0 row A, lane 1 row B
+                    if (rr >= 0) {
+                        const uint64_t v = dbits(s_pc[rr - row0]);
+                        uint64_t* pd = xpc + (((int64_t)slot * G + g) * 2 + lane) * 2;
+                        st_sc1(pd, tag | (uint32_t)v);
+                        st_sc1(pd + 1, tag | (uint32_t)(v >> 32));
+                    }
+                }
             }
             if (lane == 0) {
                 uint64_t* rec = xrec + ((int64_t)slot * G + g) * kResRecWords;
@@ -355,6 +390,17 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
             }
 #pragma unroll
             for (int q = 0; q < kResRecWords; ++q) s_rec[tid][q] = (uint32_t)w[q];
+        }
+        if (OVL && lag && wid >= kResPollers / kWave) {
+            // E2 of step s-1 on the twelve non-polling waves: own rows, every column but "-b"
+            // (E1 did it), (row, 64-column) units
+            constexpr int NW = kResWaves - kResPollers / kWave;
+            for (int u = wid - kResPollers / kWave; u < nl * nch; u += NW) {   // wave-uniform
+                const int l = u / nch, j = (u - l * nch) * kWave + lane;
+                if (j < C && j != m)
+                    s_T[l * ldl + j] = updp(l == rp_local, j == cp, s_T[l * ldl + j], s_prow[j],
+                                            s_pc[l]);
+            }
         }
         if (wid < kResPollers / kWave) {   // waves holding records (tid < G)
             const bool mine = tid < G;
@@ -434,6 +480,29 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
         // ---- D: stage the pivot row, snapshot column c, bookkeeping ----------------------------
         const int r = d.r, c = d.c;
         const uint64_t* src = xrow + (((int64_t)slot * G + d.owner) * 2 + d.rowsel) * ldg;
+        // OVL: the owner published T_{s-1} values (its "-b" entry already T_s) and the row's
+        // step s-1 pivot-column entry; upd_{s-1} is applied while staging, in place (each lane
+        // reads s_prow[j] = row s-1's value and writes row s's)
+        double pcr = 0.0;
+        const bool isr = d.r == rp;
+        if (OVL && lag) {
+            const uint64_t* ps = xpc + (((int64_t)slot * G + d.owner) * 2 + d.rowsel) * 2;
+            uint64_t lo = ld_sc1(ps), hi = ld_sc1(ps + 1);
+            if ((uint32_t)(lo >> 32) != want || (uint32_t)(hi >> 32) != want) {
+                const int64_t t0 = rt_now();
+                for (;;) {   // bounded like every spin
+                    __builtin_amdgcn_s_sleep(1);
+                    lo = ld_sc1(ps);
+                    hi = ld_sc1(ps + 1);
+                    if ((uint32_t)(lo >> 32) == want && (uint32_t)(hi >> 32) == want) break;
+                    if (rt_now() - t0 > g_res_spin_ticks || *(volatile int*)&s_err) {
+                        s_err = 1;
+                        break;
+                    }
+                }
+            }
+            pcr = bitsd((lo & 0xffffffffull) | (hi << 32));
+        }
         for (int j = tid; j < C; j += NT) {
             uint64_t lo = ld_sc1(src + 2 * j), hi = ld_sc1(src + 2 * j + 1);
             if ((uint32_t)(lo >> 32) != want || (uint32_t)(hi >> 32) != want) {
@@ -449,7 +518,8 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                     }
                 }
             }
-            s_prow[j] = bitsd((lo & 0xffffffffull) | (hi << 32));
+            const double pv = bitsd((lo & 0xffffffffull) | (hi << 32));
+            s_prow[j] = (OVL && lag && j != m) ? updp(isr, j == cp, pv, s_prow[j], pcr) : pv;
         }
         for (int i = tid; i <= rpw; i += NT)
             if (i < nl || i == fl) s_pc[i] = s_T[i * ldl + c];
@@ -483,7 +553,19 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                                               : (isc ? x : t);      // steps 2, 4 (:159-175)
             return fd_div(num, fd);
         };
-        if (ur == 0) {   // kResWaves % nch == 0: wave wid owns chunk wid % nch
+        if constexpr (OVL) {
+            // E1: the f-row and the "-b" column now; the rest (E2) during the next poll
+            for (int j = tid; j < C; j += NT)
+                s_T[fl * ldl + j] = upd(fl, j == c, s_T[fl * ldl + j], s_prow[j], s_pc[fl]);
+            for (int l = tid; l < nl; l += NT)
+                s_T[l * ldl + m] = upd(l, m == c, s_T[l * ldl + m], s_prow[m], s_pc[l]);
+            lag = true;
+            rp_local = r_local;
+            rp = r;
+            cp = c;
+            ep = e;
+            fdp = fd;
+        } else if (ur == 0) {   // kResWaves % nch == 0: wave wid owns chunk wid % nch
             const int j = (wid - (wid / nch) * nch) * kWave + lane;
             const bool jok = j < C, isc = j == c;
             const double pr = jok ? s_prow[j] : 0.0;

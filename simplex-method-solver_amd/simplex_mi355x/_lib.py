@@ -63,7 +63,7 @@ EXPORTS = (
     "smx_shard_finish", "smx_shard_fused_prime", "smx_shard_fused_begin",
     "smx_shard_fused_finish", "smx_fused_publish", "smx_shard_ahead", "smx_shard_sweep",
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
-    "smx_tune_resident", "smx_tune_resident_timeout", "smx_resident_trace", "smx_resident_bytes",
+    "smx_tune_resident", "smx_tune_resident_overlap", "smx_tune_resident_timeout", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check", "smx_fastdiv_check_bounded",
     "smx_tune_block", "smx_tune_block_pipe", "smx_tune_block_form", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
@@ -137,6 +137,7 @@ def load():
         "smx_shard_folds_pack": ([sp], ctypes.c_int),
         "smx_tune_fold": ([i64], ctypes.c_int64),
         "smx_tune_resident": ([i32], ctypes.c_int),
+        "smx_tune_resident_overlap": ([i32], ctypes.c_int),
         "smx_tune_resident_timeout": ([i64], ctypes.c_int64),
         "smx_resident_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
         "smx_resident_trace": ([vp, i32], ctypes.c_int),
@@ -213,6 +214,12 @@ def resident_plan(shape) -> tuple[int, tuple[int, int, int, int]] | None:
     if nbytes <= 0:
         return None
     return int(nbytes), tuple(int(x) for x in plan)
+
+
+def tune_resident_overlap(on: int = -1) -> int:
+    """smx_tune_resident_overlap: 1 the overlapped resident loop (default), 0 the round-3 loop,
+    -1 query only; returns the previous setting."""
+    return int(load().smx_tune_resident_overlap(on))
 
 
 def tune_resident(workgroups: int = -2) -> int:

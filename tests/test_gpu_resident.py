@@ -307,3 +307,34 @@ def test_two_resident_chains_on_separate_streams(resident_mode):
         assert np.array_equal(d.read_log(0, done), log)
         got = d.download()
         assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+
+
+@pytest.mark.parametrize("kind,n,m,k", [
+    ("uniform", 1023, 1023, 300),
+    ("mixed", 700, 650, 250),          # phase 1 rows, published before their bulk update
+    ("degenerate", 511, 511, 200),
+    ("uniform", 5, 4095, 40),
+])
+def test_resident_round3_loop_vs_overlapped(resident_mode, kind, n, m, k):
+    """smx_tune_resident_overlap(0) (every step fully updated before the next record) and the
+    default overlapped loop (bulk update under the next hand-off): same pivots, same table bits,
+    both equal to the C oracle."""
+    from oracle import c_oracle
+    from simplex_mi355x import _lib, lp
+    import simplex
+    resident_mode(0)
+    T = lp.dense_tableau(kind, 5, n, m)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    prev = _lib.tune_resident_overlap(-1)
+    try:
+        for ovl in (0, 1):
+            _lib.tune_resident_overlap(ovl)
+            sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+            assert sm._dev.resident_plan() is not None
+            sm.solve(record_history=False, max_pivots=k, chunk=k)
+            assert sm.pivot_log == [tuple(map(int, x)) for x in log], ovl
+            got = sm._dev.download()
+            assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64)), ovl
+            assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64)), ovl
+    finally:
+        _lib.tune_resident_overlap(prev)

@@ -72,31 +72,36 @@ def main():
     ap.add_argument("--k", type=int, default=400)
     ap.add_argument("--kind", default="uniform")
     ap.add_argument("--trace", action="store_true")
+    ap.add_argument("--overlap", default="1", help="smx_tune_resident_overlap settings, e.g. 0,1")
+    ap.add_argument("--seeds", default="0")
     a = ap.parse_args()
     from simplex_mi355x import _lib, lp
     from simplex_mi355x.device import DeviceTableau
-    for size in [int(x) for x in a.sizes.split(",")]:
+    for size, seed in [(int(x), int(sd)) for x in a.sizes.split(",") for sd in a.seeds.split(",")]:
         n = m = size - 1
-        T = lp.dense_tableau(a.kind, 0, n, m)
+        T = lp.dense_tableau(a.kind, seed, n, m)
         dev = DeviceTableau(T, n, m, m, log_cap=1 << 16)
         dev._host = T
         dev.resident = False
         us, ok = timed(dev, a.k)
-        print(json.dumps({"size": size, "mode": "chain", "us_per_pivot": us, "valid": ok}),
-              flush=True)
+        print(json.dumps({"size": size, "seed": seed, "mode": "chain", "us_per_pivot": us,
+                          "valid": ok}), flush=True)
         dev.resident = None
-        for wg in [int(x) for x in a.wgs.split(",")]:
+        for wg, ovl in [(int(x), int(o)) for x in a.wgs.split(",") for o in a.overlap.split(",")]:
             _lib.tune_resident(wg)
+            _lib.tune_resident_overlap(ovl)
             plan = dev.resident_plan()
             if plan is None:
                 continue
             us, ok = timed(dev, a.k)
-            rec = {"size": size, "mode": "resident", "wg": plan[1][0], "rows_per_wg": plan[1][1],
+            rec = {"size": size, "seed": seed, "mode": "resident", "overlap": ovl,
+                   "wg": plan[1][0], "rows_per_wg": plan[1][1],
                    "ept": plan[1][2], "lds": plan[1][3], "us_per_pivot": us, "valid": ok}
             if a.trace and a.k >= 170:
                 rec["anatomy_us"] = anatomy(dev, a.k, plan[1][0])
             print(json.dumps(rec), flush=True)
         _lib.tune_resident(0)
+        _lib.tune_resident_overlap(1)
         dev.close()
 
 
