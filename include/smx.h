@@ -295,10 +295,11 @@ int64_t smx_tune_resident_timeout(int64_t ticks);
  * smx_resident_trace (diagnostic): device buffer of 64 x G x 8 uint64 s_memrealtime stamps for
  * steps from_step .. from_step+63 of later launches (NULL disables). */
 int smx_tune_resident(int32_t workgroups);
-/* smx_tune_resident_overlap: 1 (default) the overlapped resident loop -- step s's bulk update
- * runs on the non-polling waves during step s+1's hand-off, the records read T_{s+1} on the fly
- * -- 0 the round-3 loop (every step fully updated before the next record); -1 query only;
- * returns the previous setting.  Bit-identical either way. */
+/* smx_tune_resident_overlap: 2 (default) automatic -- the overlapped resident loop from 768
+ * columns: step s's bulk update runs on the non-polling waves during step s+1's hand-off, the
+ * records read T_{s+1} on the fly -- 1 always overlapped, 0 the round-3 loop (every step fully
+ * updated before the next record); -1 query only; returns the previous setting.  Bit-identical
+ * either way. */
 int smx_tune_resident_overlap(int32_t on);
 int smx_resident_trace(void* trace, int32_t from_step);
 int64_t smx_resident_bytes(const smx_shape* shape, int32_t* plan_out);

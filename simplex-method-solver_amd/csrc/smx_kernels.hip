@@ -320,9 +320,12 @@ struct ResPlan {
     int G, rpw, ept;
     int64_t lds, rec_bytes, row_off, pc_off, bytes;
 };
-// 1: the overlapped loop (k_resident<true>: the bulk update hidden under the next hand-off's
-// poll); 0: the round-3 loop (smx_tune_resident_overlap)
-int g_resident_ovl = 1;
+// The overlapped loop (k_resident<true>: the bulk update hidden under the next hand-off's poll)
+// or the round-3 loop (smx_tune_resident_overlap): 2 automatic -- overlapped from 768 columns
+// (tools/resident_bench.py, profiles/r04k/: 1024^2 8.8-9.0 vs 9.6-9.7 us per pivot over seeds
+// 0..4, 1536^2 10.4 vs 13.4; 512^2 7.5 vs 7.3, where the update it hides is short); 1 / 0 forced.
+int g_resident_ovl = 2;
+constexpr int kResOvlMinCols = 768;
 
 bool resident_plan(const smx_shape& s, ResPlan* p) {
     if (g_resident < 0) return false;
@@ -366,7 +369,8 @@ int launch_resident_kernel(double* buf0, double* buf1, const smx_shape& s, const
         }
         attr = true;
     }
-    hipLaunchKernelGGL(g_resident_ovl ? k_resident<true> : k_resident<false>, dim3(p.G),
+    const bool ovl = g_resident_ovl == 1 || (g_resident_ovl == 2 && s.m + 1 >= kResOvlMinCols);
+    hipLaunchKernelGGL(ovl ? k_resident<true> : k_resident<false>, dim3(p.G),
                        dim3(kResBlock), (size_t)p.lds, st, buf0, buf1,
                        s.ld, s.n, s.m, s.flen, fscan_of(s), parity, k, p.rpw, ctl, log, xhist,
                        log_cap, reinterpret_cast<uint64_t*>(xch),
@@ -1439,7 +1443,7 @@ int smx_shard_finish(const double* Tin, double* Tout, const double* recv, int32_
 
 int smx_tune_resident_overlap(int32_t on) {
     const int prev = g_resident_ovl;
-    if (on >= 0) g_resident_ovl = on ? 1 : 0;
+    if (on >= 0 && on <= 2) g_resident_ovl = on;
     return prev;
 }
 

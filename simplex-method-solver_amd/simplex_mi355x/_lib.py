@@ -217,8 +217,8 @@ def resident_plan(shape) -> tuple[int, tuple[int, int, int, int]] | None:
 
 
 def tune_resident_overlap(on: int = -1) -> int:
-    """smx_tune_resident_overlap: 1 the overlapped resident loop (default), 0 the round-3 loop,
-    -1 query only; returns the previous setting."""
+    """smx_tune_resident_overlap: 2 automatic (overlapped from 768 columns, the default), 1 the
+    overlapped resident loop, 0 the round-3 loop, -1 query only; returns the previous setting."""
     return int(load().smx_tune_resident_overlap(on))
 
 

@@ -325,7 +325,7 @@ def test_resident_round3_loop_vs_overlapped(resident_mode, kind, n, m, k):
     resident_mode(0)
     T = lp.dense_tableau(kind, 5, n, m)
     Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
-    prev = _lib.tune_resident_overlap(-1)
+    prev = _lib.tune_resident_overlap(-1)   # (2: automatic)
     try:
         for ovl in (0, 1):
             _lib.tune_resident_overlap(ovl)

@@ -101,7 +101,7 @@ def main():
                 rec["anatomy_us"] = anatomy(dev, a.k, plan[1][0])
             print(json.dumps(rec), flush=True)
         _lib.tune_resident(0)
-        _lib.tune_resident_overlap(1)
+        _lib.tune_resident_overlap(2)
         dev.close()
 
 
