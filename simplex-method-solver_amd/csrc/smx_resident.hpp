@@ -483,34 +483,26 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
         // OVL: the owner published T_{s-1} values (its "-b" entry already T_s) and the row's
         // step s-1 pivot-column entry; upd_{s-1} is applied while staging, in place (each lane
         // reads s_prow[j] = row s-1's value and writes row s's)
-        // (the entry's granules are loaded together with the row's first granules and checked
-        // after them: one round trip for both)
         double pcr = 0.0;
-        bool pc_ok = !(OVL && lag);
         const bool isr = d.r == rp;
-        const uint64_t* ps = xpc + (((int64_t)slot * G + d.owner) * 2 + d.rowsel) * 2;
-        uint64_t plo = 0, phi = 0;
-        if (!pc_ok) {
-            plo = ld_sc1(ps);
-            phi = ld_sc1(ps + 1);
-        }
-        auto pc_wait = [&]() {
-            if ((uint32_t)(plo >> 32) != want || (uint32_t)(phi >> 32) != want) {
+        if (OVL && lag) {
+            const uint64_t* ps = xpc + (((int64_t)slot * G + d.owner) * 2 + d.rowsel) * 2;
+            uint64_t lo = ld_sc1(ps), hi = ld_sc1(ps + 1);
+            if ((uint32_t)(lo >> 32) != want || (uint32_t)(hi >> 32) != want) {
                 const int64_t t0 = rt_now();
                 for (;;) {   // bounded like every spin
                     __builtin_amdgcn_s_sleep(1);
-                    plo = ld_sc1(ps);
-                    phi = ld_sc1(ps + 1);
-                    if ((uint32_t)(plo >> 32) == want && (uint32_t)(phi >> 32) == want) break;
+                    lo = ld_sc1(ps);
+                    hi = ld_sc1(ps + 1);
+                    if ((uint32_t)(lo >> 32) == want && (uint32_t)(hi >> 32) == want) break;
                     if (rt_now() - t0 > g_res_spin_ticks || *(volatile int*)&s_err) {
                         s_err = 1;
                         break;
                     }
                 }
             }
-            pcr = bitsd((plo & 0xffffffffull) | (phi << 32));
-            pc_ok = true;
-        };
+            pcr = bitsd((lo & 0xffffffffull) | (hi << 32));
+        }
         for (int j = tid; j < C; j += NT) {
             uint64_t lo = ld_sc1(src + 2 * j), hi = ld_sc1(src + 2 * j + 1);
             if ((uint32_t)(lo >> 32) != want || (uint32_t)(hi >> 32) != want) {
@@ -526,7 +518,6 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                     }
                 }
             }
-            if (!pc_ok) pc_wait();
             const double pv = bitsd((lo & 0xffffffffull) | (hi << 32));
             s_prow[j] = (OVL && lag && j != m) ? updp(isr, j == cp, pv, s_prow[j], pcr) : pv;
         }
