@@ -155,6 +155,7 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
     __shared__ ResWave s_wred[kResPollers / kWave];
     __shared__ int s_err;
     __shared__ int s_cfu;
+    __shared__ int s_rab[2];   // OVL: local candidate rows A / B of this step (-1: none)
     constexpr int NT = kResBlock;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -339,8 +340,17 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
                         }
                     }
                 };
-                if (rb >= 0) put(dst + ldg, rb - row0);
-                if (ra >= 0) put(dst, ra - row0);
+                if constexpr (OVL) {
+                    // published by the non-polling waves during the poll (below), each chunk by
+                    // the wave whose E2 unit it is, read before that wave updates it
+                    if (lane == 0) {
+                        s_rab[0] = ra >= 0 ? ra - row0 : -1;
+                        s_rab[1] = rb >= 0 ? rb - row0 : -1;
+                    }
+                } else {
+                    if (rb >= 0) put(dst + ldg, rb - row0);
+                    if (ra >= 0) put(dst, ra - row0);
+                }
                 if (OVL && lag && lane < 2) {   // the rows' step s-1 pivot-column entries
                     const int rr = lane ? rb : ra;   // lane 0 row A, lane 1 row B
                     if (rr >= 0) {
@@ -391,15 +401,25 @@ __global__ __launch_bounds__(kResBlock) void k_resident(
 #pragma unroll
             for (int q = 0; q < kResRecWords; ++q) s_rec[tid][q] = (uint32_t)w[q];
         }
-        if (OVL && lag && wid >= kResPollers / kWave) {
-            // E2 of step s-1 on the twelve non-polling waves: own rows, every column but "-b"
-            // (E1 did it), (row, 64-column) units
+        if (OVL && wid >= kResPollers / kWave) {
+            // the twelve non-polling waves, (row, 64-column) units: the candidate rows' T_s
+            // values out as tagged granules (step s < k), then E2 of step s-1 -- every column
+            // but "-b" (E1 did it) -- each unit read before its own wave rewrites it
             constexpr int NW = kResWaves - kResPollers / kWave;
+            const int pa = s < k ? s_rab[0] : -1, pb = s < k ? s_rab[1] : -1;
+            uint64_t* dst = xrow + ((int64_t)slot * G + g) * 2 * ldg;
             for (int u = wid - kResPollers / kWave; u < nl * nch; u += NW) {   // wave-uniform
                 const int l = u / nch, j = (u - l * nch) * kWave + lane;
-                if (j < C && j != m)
-                    s_T[l * ldl + j] = updp(l == rp_local, j == cp, s_T[l * ldl + j], s_prow[j],
-                                            s_pc[l]);
+                if (j >= C) continue;
+                const double x = s_T[l * ldl + j];
+                if (l == pa || l == pb) {   // (row A is a NaN-ratio candidate, B another row)
+                    const uint64_t v = dbits(x);
+                    uint64_t* d = dst + (l == pb ? ldg : 0) + 2 * j;
+                    st_sc1(d, tag | (uint32_t)v);
+                    st_sc1(d + 1, tag | (uint32_t)(v >> 32));
+                }
+                if (lag && j != m)
+                    s_T[l * ldl + j] = updp(l == rp_local, j == cp, x, s_prow[j], s_pc[l]);
             }
         }
         if (wid < kResPollers / kWave) {   // waves holding records (tid < G)
