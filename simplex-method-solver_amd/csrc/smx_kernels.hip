@@ -24,6 +24,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <mutex>
+#include <thread>
+#include <vector>
 #include <utility>
 #include <string.h>
 
@@ -1980,6 +1982,31 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                    int32_t pivots, int32_t exchange) {
     if (!mshard_args_ok(ranks, nranks, k, pivots, exchange)) return (int)hipErrorInvalidValue;
     if (k == 0) return 0;
+    if (exchange == SMX_XCHG_RCCL) {
+        // One host thread per device, each enqueuing its rank's whole chain on its own
+        // communicator -- the multi-process protocol (launch_block_chain), no cross-device
+        // group call: one thread driving N devices spends ~5 us of host time per launch, so at
+        // 8 ranks its per-pivot enqueue (~3N launches) outgrows a rank's ~28-34 us of device
+        // work (tools/mshard_host_cost.py, profiles/r04h/, r04j/); per thread it is 3 launches.
+        std::vector<int> errs((size_t)nranks, 0);
+        std::vector<std::thread> th;
+        th.reserve((size_t)nranks);
+        for (int q = 0; q < nranks; ++q)
+            th.emplace_back([&, q] {
+                const smx_rank& R = ranks[q];
+                int e = (int)hipSetDevice(R.device);
+                if (!e)
+                    e = launch_block_chain(R.buf0, R.buf1, R.shape, parity & 1, k, pivots, R.ctl,
+                                           static_cast<char*>(R.blk), R.log, R.xhist, R.log_cap,
+                                           S(R.stream), nullptr, R.send, R.recv, nranks,
+                                           reinterpret_cast<ncclComm_t>(R.comm));
+                errs[(size_t)q] = e;
+            });
+        for (auto& t : th) t.join();
+        for (int e : errs)
+            if (e) return e;
+        return 0;
+    }
     return mshard_enqueue(ranks, nranks, parity, k, pivots, exchange);
 }
 

@@ -166,10 +166,11 @@ def test_multi_pick_is_read_only():
 @pytest.mark.parametrize("light", [0, 1])
 def test_multi_rccl_exchange_world1_vs_oracle(light):
     """The branch a real multi-GPU node takes (distinct devices -> exchange="rccl"), run at world
-    size 1: ncclCommInitAll on one device, then per pivot the grouped all-gather of the send
-    slots (full, smx_tune_shard_xchg(0)) or the header all-gather + k_bsh_pick + the grouped
-    int64 MAX all-reduce of the pivot row (light, smx_tune_shard_xchg(1)); smx_mshard_run,
-    reached from SimplexMethod(..., devices=[0], exchange="rccl") as main.py:313 would call it.
+    size 1: ncclCommInitAll on one device, then one host thread per device enqueuing its rank's
+    chain on its own communicator: per pivot the all-gather of the send slots (full,
+    smx_tune_shard_xchg(0)) or the header all-gather + k_bsh_pick + the int64 MAX all-reduce of
+    the pivot row (light, smx_tune_shard_xchg(1)); smx_mshard_run, reached from
+    SimplexMethod(..., devices=[0], exchange="rccl") as main.py:313 would call it.
     Pivot log and the whole table bit for bit against the C oracle, then the reference's own
     example LP through get_solution()."""
     import simplex

@@ -30,6 +30,8 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=48)
     ap.add_argument("--pivots", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--exchange", default=None, help="copy (default on one device) or rccl "
+                    "(one host thread per device; one rank per device, so world 1 here)")
     a = ap.parse_args()
     import torch
     from simplex_mi355x import lp
@@ -37,7 +39,7 @@ def main() -> None:
     n = m = a.size - 1
     T = lp.dense_tableau("uniform", 0, n, m)
     for world in (int(x) for x in a.ranks.split(",")):
-        mt = MultiTableau(T, n, m, m, ["cuda:0"] * world, pivots=a.pivots)
+        mt = MultiTableau(T, n, m, m, ["cuda:0"] * world, pivots=a.pivots, exchange=a.exchange)
         mt.run(a.pivots, graph=False)   # warm-up: prime, first kernels
         mt.sync_state()
         logs = {}
