@@ -617,8 +617,9 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
         grid = update_grid(s, (const void*)blk_sweep_fn(P, 4), 0, 5);
         if (((int64_t)grid * kUpdWaves) % nchunks != 0) form = 5;
     }
-    if (form == 5)   // 8 blocks per CU (P = 16-24 at 64-96 VGPRs, profiles/r04b/lab2.jsonl)
-        grid = sweep_grid_lds(s, 8);
+    if (form == 5)   // 8 blocks per CU (P = 16-24 at 64-96 VGPRs, profiles/r04b/lab2.jsonl);
+                     // smx_tune_set(-2, bpc) overrides it (A/B timing)
+        grid = sweep_grid_lds(s, g_blocks_per_cu > 0 ? g_blocks_per_cu : 8);
     BlkSweepFn fn = blk_sweep_fn(P, form);
     BlkHdr* hs = reinterpret_cast<BlkHdr*>(blk);
     const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk + kBlkHdrBytes * slot);
