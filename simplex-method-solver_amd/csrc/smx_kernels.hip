@@ -441,12 +441,22 @@ int g_block = 0;
 constexpr int64_t kBlockMinTable = 48ll << 20;
 constexpr int64_t kBlockWideTable = 256ll << 20;
 
+// Round 4: tables of 1-4 GiB take up to 20 pivots per sweep (the LDS layout past 12,
+// k_blk_sweep<P, 5>): at 16384^2 the per-pivot cost is flat from 12 to 20 (99.4 / 101.5 / 99.1 us
+// at 12 / 16 / 20, profiles/r04r/; 100.8 / 98.4 / 97.8 on another box, profiles/r04e/), so the
+// larger bound only changes how a chain is cut -- 20 pivots become ONE sweep of 20 instead of two
+// of 10 (106.8 us per pivot at 10).  Beyond 4 GiB (config 5's 17 GB) and below 1 GiB (8192^2:
+// 32.0 / 33.6 / 36.1 us at 12 / 14 / 16, where the planner's share is larger) it stays at 12.
+constexpr int64_t kBlockHugeTable = 1ll << 30;
+constexpr int64_t kBlockHugeTableMax = 4ll << 30;
+
 int block_pivots(const smx_shape& s) {
     if (g_block == 1) return 0;
     if (s.row0 != 0 || s.rows != s.n || s.rows < 1 || s.m < 1) return 0;   // unsharded only
     if (g_block >= 2) return g_block;
     const int64_t bytes = (int64_t)(s.rows + 1) * s.ld * 8;
     if (bytes < kBlockMinTable) return 0;
+    if (bytes >= kBlockHugeTable && bytes < kBlockHugeTableMax) return 20;
     return bytes >= kBlockWideTable ? 12 : 10;
 }
 

@@ -396,7 +396,9 @@ def rank_block_pivots(rows: int, m: int) -> int:
     ld = -(-(m + 1) // 16) * 16
     shape = [ld, rows, rows, m, m, 0, _lib.load().smx_nparts_for(rows, m)]
     plan = _lib.block_plan(shape, 0) if rows >= 1 else None
-    return plan[1] if plan is not None else 8
+    # at most 12 per sweep on a rank: the sharded planner's per-pivot exchange makes its share
+    # larger than the single-GPU policy's 1-4 GiB band (20) was measured for
+    return min(plan[1], 12) if plan is not None else 8
 
 
 def run_block_protocol(be, k: int, exchange, pivots: int | None = None, reduce_row=None,
