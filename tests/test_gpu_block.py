@@ -242,11 +242,13 @@ def test_block_terminal_state_matches_chain(block_mode):
     assert seen > 10
 
 
-@pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 23, 12), (16383, 16383, 9, 12),
-                                     (16383, 16383, 20, 12), (3071, 3071, 13, 10)])
+@pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 23, 12), (16383, 16383, 9, 20),
+                                     (16383, 16383, 20, 20), (16383, 16383, 47, 20),
+                                     (3071, 3071, 13, 10)])
 def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
-    """BASELINE sizes through the default policy (10 or 12 pivots per sweep at most, blocks of
-    near-equal size: 23 = 12 + 11, 9 = one block, 20 = 10 + 10, 13 = 7 + 6)."""
+    """BASELINE sizes through the default policy (10, 12 or -- 1-4 GiB tables -- 20 pivots per
+    sweep at most, blocks of near-equal size: 23 = 12 + 11, 9 = one block, 20 = one block of 20
+    in the LDS layout (k_blk_sweep<20, 5>), 47 = 16 + 16 + 15, 13 = 7 + 6)."""
     from simplex_mi355x import lp, _lib
     from simplex_mi355x.device import DeviceTableau
     from oracle import c_oracle
