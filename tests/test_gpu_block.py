@@ -269,7 +269,9 @@ def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
 def test_block_plan_policy(block_mode):
     from simplex_mi355x import _lib
     block_mode(0)
-    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 12
+    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 20   # 1-4 GiB
+    assert _lib.block_plan([32768, 32767, 32767, 32767, 32767, 0, 64])[1] == 12   # 8 GiB
+    assert _lib.block_plan([32768, 65535, 65535, 32767, 32767, 0, 64])[1] == 12   # config 5
     assert _lib.block_plan([8192, 8191, 8191, 8191, 8191, 0, 32])[1] == 12
     assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 10
     assert _lib.block_plan([2048, 2047, 2047, 2047, 2047, 0, 8]) is None    # below 48 MiB
