@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r04s
 mkdir -p $O
 cd $R
-timeout -k 10 900 python -u -m pytest tests/test_gpu_block.py tests/test_gpu_configs.py tests/test_gpu_block_sharded.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_block.py tests/test_gpu_block_pipe.py tests/test_gpu_configs.py tests/test_gpu_block_sharded.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/pytest.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err || exit $?
