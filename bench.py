@@ -99,6 +99,10 @@ def parse():
                     help="row-sharded block path: exchange per pivot (full = all-gather of every "
                          "rank's header + 2 candidate rows; light = header all-gather + one "
                          "max all-reduce of the pivot row; auto = light from 4 ranks on)")
+    ap.add_argument("--sustained", type=int, default=200,
+                    help="block path, N = 1: after the timed region, time this many further "
+                         "pivots with HIP events around every sweep (the steady-state rate beside "
+                         "the timed burst), then one more block after 1 s idle; 0 = off")
     ap.add_argument("--enqueue-probe", action="store_true",
                     help="row-sharded block path: after the timed region, time the host enqueue "
                          "per pivot of the eager and graph-captured chains (host_enqueue)")
@@ -294,6 +298,37 @@ def _single_pivot_line(dev, R, C, k):
             "unit": "GB/s", "frac": ach / PEAK_HBM_GBS}
 
 
+def sustained_record(dev, P, k, idle_s=1.0):
+    """The steady state beside the timed burst (outside the timed region, continuing the same
+    trajectory): k more pivots in blocks of at most P with HIP events around every sweep, then,
+    after `idle_s` seconds with the GPU idle, one more block of P.  A sweep that is slower in the
+    sustained run than in the burst but fast again after the pause points at the clock (power /
+    thermal state under a long fp64 load); one that stays slow points at the data (units leaving
+    the sweep's fast path as the table's values spread)."""
+    import numpy as np
+    from simplex_mi355x import _lib
+    L = _lib.load()
+    nb = -(-k // P)
+    _lib.check(L.smx_timer_reserve(2 * nb + 2), "smx_timer_reserve")
+    t0 = time.perf_counter()
+    sw, tot = dev.run_block_timed(k, P)
+    wall = time.perf_counter() - t0
+    ctl = dev.sync_state()
+    out = {"pivots": k, "pivots_s": k / (tot * 1e-3), "wall_pivots_s": k / wall,
+           "device_ms": tot, "sweeps": len(sw), "sweep_ms": [round(float(x), 4) for x in sw],
+           "mean_sweep_ms": float(np.mean(sw)), "first_sweep_ms": float(sw[0]),
+           "last_sweep_ms": float(sw[-1]),
+           "planner_ms_per_pivot": (tot - float(np.sum(sw))) / k,
+           "trajectory_valid": not bool(ctl["term"])}
+    if not ctl["term"]:
+        time.sleep(idle_s)
+        sw2, tot2 = dev.run_block_timed(P, P)
+        ctl = dev.sync_state()
+        out["after_idle"] = {"idle_s": idle_s, "pivots": P, "sweep_ms": float(sw2[0]),
+                             "device_ms": tot2, "trajectory_valid": not bool(ctl["term"])}
+    return out
+
+
 def run_single(args):
     import numpy as np
     import torch
@@ -387,6 +422,9 @@ def run_single(args):
         # whether HBM or the caches bound it
         achieved = physical_check(kernel, bytes_per_sweep, avg_kernel, 8.0 * R * C)
     workload =f"{R}x{C} dense fp64 tableau, {args.kind} random LP seed {args.seed}"
+    sustained = None
+    if bplan is not None and valid and args.sustained > 0:
+        sustained = sustained_record(dev, bplan[1], args.sustained)
     copy_gbs = copy_ceiling(8.0 * R * C)   # same bytes as one sweep (outside timing)
     single = None
     if bplan is not None and valid:
@@ -421,6 +459,7 @@ def run_single(args):
                           "copy_ceiling_gbs": copy_gbs, "frac_of_copy": achieved / copy_gbs},
                          **extra),
         "single_pivot_update": single,
+        "sustained": sustained,
         "trajectory_valid": bool(valid),
         "basis_cycle": cycle,
     }

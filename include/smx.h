@@ -261,6 +261,9 @@ int smx_shard_sweep(const double* Tin, double* Tout, const double* recv, int32_t
 int smx_comm_unique_id(void* id_out /* 128 bytes */);
 int smx_comm_init(void** comm_out, int32_t nranks, const void* id, int32_t rank);
 int smx_comm_destroy(void* comm);
+/* What RCCL formed: the communicator's rank count (ncclCommCount), this rank (ncclCommUserRank)
+ * and its device (ncclCommCuDevice) -- the multi-GPU bench line records them for every rank. */
+int smx_comm_info(void* comm, int32_t* count, int32_t* rank, int32_t* device);
 int smx_shard_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
                   smx_ctl* ctl, smx_part* parts, double* send, double* recv, int32_t nranks,
                   void* comm, int32_t* log, int64_t log_cap, void* stream);
@@ -321,9 +324,16 @@ int smx_fastdiv_check(const double* num, const double* den, int64_t count,
  * long[4].  Test support. */
 int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t count,
                               unsigned long long* out, void* stream);
+/* Diagnostic: the block sweep's units (one row x 128 columns) per path, summed over every
+ * k_blk_sweep launch since the last clear -- out[0..count) = fast, zero-extended, window-tracked,
+ * window vote failed (-> exact), exact directly, units in chunks not free / not zero-safe, units of
+ * rows flagged 0 / 3, inputs out of bounds on a free chunk and flag-1 row (smx_block.hpp kPc*).
+ * Synchronises the device.  Returns the number of counters, or -hipErrorNotSupported in the
+ * product build (the counters exist only in libsmx_diag.so, `make -C csrc diag`). */
+int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear);
 
 /* ---- block pivots: P pivots per HBM sweep ------------------------------------------------
- * k pivots of the get_solution loop (simplex.py:184-198) in blocks of `pivots` (1..16): per block,
+ * k pivots of the get_solution loop (simplex.py:184-198) in blocks of `pivots` (1..24): per block,
  * `pivots` planning steps each decide one pivot (pick_element, simplex.py:70-141) from the block's
  * input table T_k -- every value of T_{k+l} they need is re-derived from T_k with the update's own
  * expression chained l times -- then ONE sweep applies all of them to every element
@@ -333,9 +343,9 @@ int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t coun
  * is in buf[(parity + d) & 1] (the sweep works in place when a block applies an even count).
  * Unsharded tableaux only (row0 = 0, rows = n).  `blk` is device scratch of smx_block_bytes
  * bytes (no initialisation needed).  smx_block_bytes: with *pivots_inout = 0 it asks the
- * library's policy (smx_tune_block: 0 automatic = 6 pivots for tables of 48..256 MiB, 10
- * up to 1 GiB, 12 beyond; 1 never, 2..16 that many) and returns 0 when chains of `shape` would not use blocks; with 1..16 it asks for
- * that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
+ * library's policy (smx_tune_block: 0 automatic = 10 pivots for tables of 48..256 MiB, 12 from
+ * 256 MiB, 20 for 1..4 GiB, 12 beyond; 1 never, 2..24 that many) and returns 0 when chains of
+ * `shape` would not use blocks; with 1..24 it asks for that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
  * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
  * entries) and the chain's total. */
 int smx_tune_block(int32_t pivots);
@@ -434,17 +444,24 @@ int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, sm
                        void* blk, int64_t blk_bytes, void* stream);
 
 /* ---- row sharding across the devices of ONE process (SimplexMethod(..., devices=[...])) ------
- * The block protocol of smx_bshard_* for all ranks of a single-process job, driven by one host
- * thread: every rank is a row block on its own device and stream (the smx_bshard_* buffers of
- * that rank), and per pivot the ranks exchange their send slots by
- *   SMX_XCHG_RCCL -- one grouped ncclAllGather over the communicators of smx_mshard_comms
- *                    (ncclCommInitAll over distinct devices), or
- *   SMX_XCHG_COPY -- device copies of every send slot into every recv, ordered by events (any
- *                    devices, also several ranks on ONE device, where RCCL refuses).
+ * The block protocol of smx_bshard_* for all ranks of a single-process job: every rank is a row
+ * block on its own device and stream (the smx_bshard_* buffers of that rank), and per pivot the
+ * ranks exchange their send slots by
+ *   SMX_XCHG_RCCL -- the communicators of smx_mshard_comms (ncclCommInitAll over distinct
+ *                    devices); one host thread per rank enqueues that rank's whole chain with
+ *                    its own collectives, exactly as a rank of a multi-process job does.  Should
+ *                    any rank fail to enqueue, every communicator is aborted (ncclCommAbort, so
+ *                    no rank waits forever for the failed one's collectives) and the call returns
+ *                    SMX_ERR_COMMS_ABORTED: the handles are gone, do not destroy them;
+ *   SMX_XCHG_COPY -- one host thread; device copies of every send slot into every recv (one
+ *                    gather launch per pivot on rank 0's stream when all ranks share a device),
+ *                    ordered by events (any devices, also several ranks on ONE device, where
+ *                    RCCL refuses).
  * Stream-ordered, no host synchronisation; the per-rank state afterwards is exactly what
  * smx_bshard_run leaves on each rank of a multi-process job. */
 #define SMX_XCHG_RCCL 0
 #define SMX_XCHG_COPY 1
+#define SMX_ERR_COMMS_ABORTED (-2000)
 typedef struct smx_rank {
     int32_t device;     /* HIP device ordinal of this row block                              */
     int32_t reserved;

@@ -1333,6 +1333,40 @@ __device__ __forceinline__ dbl2 blk_exact_h(dbl2 v, int row, int j, const BlkHdr
 //     VGPRs at any P, so 16-24 pivots per sweep keep 7-8 waves per SIMD instead of spilling
 //     scalars (tools/sweep_lab2.hip V3 / V6, profiles/r04b/lab2.jsonl: P = 20 1.33 ms vs 1.43 ms
 //     for the register layout at 16384^2).
+// Diagnostic build only (-DSMX_PATH_COUNT, Makefile target `diag` -> libsmx_diag.so): how many
+// (row, 128-column chunk) units of the flag-form sweep take each path, summed over every launch
+// until smx_diag_path_counts reads (and optionally clears) them.  Per wave in registers, one add
+// per counter and wave at the end (lane k adds counter k).  The product build has none of it.
+enum : int {
+    kPcFast = 0,        // chunk_free, row flag 1, bounded inputs: the unchecked fast path
+    kPcZero,            // the zero-extended domain (fd_zero)
+    kPcWindow,          // the window-tracked path, vote passed
+    kPcWindowFail,      // the window-tracked path, vote failed -> exact
+    kPcExact,           // straight to the exact path (a pivot row, or a pivot not ok)
+    kPcChunkNotFree,    // units in chunks that are not chunk_free (e / pivot-row values)
+    kPcChunkNotZok,     // units in chunks that are not even chunk_zok
+    kPcRowFlag0,        // units of rows with flag 0 (a multiplier unbounded, not zero)
+    kPcRowFlag3,        // units of rows with flag 3 (bounded or zero, at least one zero)
+    kPcXFail,           // chunk_free and flag 1, but an input element out of bounds
+    kPcCount
+};
+#ifdef SMX_PATH_COUNT
+__device__ unsigned long long g_path_cnt[kPcCount];
+#define SMX_PC_DECL uint32_t pc_cnt[kPcCount] = {};
+#define SMX_PC(k) (++pc_cnt[(k)])
+#define SMX_PC_FLUSH                                                                            \
+    do {                                                                                        \
+        const int l_ = threadIdx.x & (kWave - 1);                                               \
+        uint32_t v_ = 0;                                                                        \
+        _Pragma("unroll") for (int k_ = 0; k_ < kPcCount; ++k_) if (l_ == k_) v_ = pc_cnt[k_];  \
+        if (l_ < kPcCount && v_) atomicAdd(&g_path_cnt[l_], (unsigned long long)v_);            \
+    } while (0)
+#else
+#define SMX_PC_DECL
+#define SMX_PC(k) ((void)0)
+#define SMX_PC_FLUSH ((void)0)
+#endif
+
 template <int P, int FORM>
 __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* Tout, int64_t ld,
                                                     int R, int C, const BlkHdr* __restrict__ h,
@@ -1393,6 +1427,7 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         else return dbl2{eq[q], yq[q]};
     };
     const bool kNoFree = g_blk_nofree != 0;
+    SMX_PC_DECL
     uint32_t et = 0, pt = 0;
     bool zok = true;   // every pivot-row value bounded or an exact +-0
 #pragma unroll
@@ -1438,7 +1473,15 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         bool ok = false;
         const uint32_t xt = max((uint32_t)__double2hiint(x0[0]) << 1,
                                 (uint32_t)__double2hiint(x0[1]) << 1);
+#ifdef SMX_PATH_COUNT
+        if (!chunk_free) SMX_PC(kPcChunkNotFree);
+        if (!chunk_zok) SMX_PC(kPcChunkNotZok);
+        if (rf == 0) SMX_PC(kPcRowFlag0);
+        if (rf == 3) SMX_PC(kPcRowFlag3);
+        if (chunk_free && rf == 1 && !__all(xt < kBndXMax)) SMX_PC(kPcXFail);
+#endif
         if (chunk_free && rf == 1 && __all(xt < kBndXMax)) {
+            SMX_PC(kPcFast);
             if constexpr (!LDS) {
                 // the 2P products p * mq first (they do not depend on the chain) and held there:
                 // issued back to back, the chains after them run without waiting on any
@@ -1490,6 +1533,7 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
             // the zero-extended domain (rf 1 or 3, a chunk or row with exact zeros): the same
             // arithmetic with fd_zero's v_div_fixup (ONE more instruction per element-pivot)
             asm volatile("" ::: "memory");   // keeps this path out of the fast path's code
+            SMX_PC(kPcZero);
 #pragma unroll
             for (int q = 0; q < P; ++q) {
                 const dbl2 p = PR(q);
@@ -1523,6 +1567,9 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                 v0 = dbl2{rr[0], rr[1]};
             }
             ok = __all(wt < kWinSpan);
+            SMX_PC(ok ? kPcWindow : kPcWindowFail);
+        } else {
+            SMX_PC(kPcExact);
         }
         if (!ok) {
             // reloaded (not written yet, even in place) so x0 need not stay live beside the
@@ -1552,6 +1599,7 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         asm volatile("s_waitcnt vmcnt(2)" : "+v"(a) :: "memory");
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    SMX_PC_FLUSH;   // every exit of the loop lands here (diagnostic build only)
 }
 
 // After a flag-form sweep: every element of every pivot column, rewritten from the planner's

@@ -182,8 +182,19 @@ int variant_for(const smx_shape& s) {
 
 // Resident blocks per CU for a kernel, cached.  The grid is exactly CUs x this, so every block
 // is resident at once and the balanced unit ranges finish together (no second residency round).
+// The host-side caches below are shared by smx_mshard_run's per-device threads: one mutex.
+std::mutex g_cache_mu;
+
+// Resident 256-thread blocks per CU of `fn` by the occupancy API (registers and LDS), one block
+// of margin below its answer, cached; at most `cap`.
+int resident_bpc(const void* fn, int cap);
+
 int blocks_per_cu(const void* fn) {
     if (g_blocks_per_cu > 0) return g_blocks_per_cu;
+    return resident_bpc(fn, kDefaultBpc);
+}
+
+int resident_bpc(const void* fn, int cap) {
     struct Entry {
         const void* fn;
         int dev;
@@ -193,8 +204,9 @@ int blocks_per_cu(const void* fn) {
     static int ncache = 0;
     int dev = 0;
     (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lock(g_cache_mu);
     for (int i = 0; i < ncache; ++i)
-        if (cache[i].fn == fn && cache[i].dev == dev) return cache[i].bpc;
+        if (cache[i].fn == fn && cache[i].dev == dev) return cache[i].bpc < cap ? cache[i].bpc : cap;
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, fn, kUpdBlock, 0) != hipSuccess ||
         bpc < 1)
@@ -202,9 +214,8 @@ int blocks_per_cu(const void* fn) {
     // ROCm 7.2 over-reports by one block/CU for 256-thread kernels above 80 SGPRs
     // (MI355X_MICROARCH.md, residency): keep one block of margin below the API's answer.
     if (bpc > 1) bpc -= 1;
-    if (bpc > kDefaultBpc) bpc = kDefaultBpc;
     if (ncache < 128) cache[ncache++] = Entry{fn, dev, bpc};
-    return bpc;
+    return bpc < cap ? bpc : cap;
 }
 
 int num_cus() {
@@ -212,6 +223,7 @@ int num_cus() {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 0 || dev >= 64) dev = 0;
+    std::lock_guard<std::mutex> lock(g_cache_mu);
     if (!cus[dev]) {
         int v = 0;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -627,10 +639,13 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
         grid = update_grid(s, (const void*)blk_sweep_fn(P, 4), 0, 5);
         if (((int64_t)grid * kUpdWaves) % nchunks != 0) form = 5;
     }
-    if (form == 5)   // 8 blocks per CU (P = 16-24 at 64-96 VGPRs, profiles/r04b/lab2.jsonl);
-                     // smx_tune_set(-2, bpc) overrides it (A/B timing)
-        grid = sweep_grid_lds(s, g_blocks_per_cu > 0 ? g_blocks_per_cu : 8);
     BlkSweepFn fn = blk_sweep_fn(P, form);
+    if (form == 5)   // as many workgroups per CU as are resident (at most 8): the P KiB of
+                     // pivot-row slices in LDS and ~106 SGPRs cap it at 7 from P = 16 (6 at 24);
+                     // a grid sized for 8 left 1/8 of the rows to a second residency round.
+                     // smx_tune_set(-2, bpc) overrides it (A/B timing)
+        grid = sweep_grid_lds(s, g_blocks_per_cu > 0 ? g_blocks_per_cu
+                                                     : resident_bpc((const void*)fn, 8));
     BlkHdr* hs = reinterpret_cast<BlkHdr*>(blk);
     const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk + kBlkHdrBytes * slot);
     const double* mul = reinterpret_cast<const double*>(blk + L.mul + slot * L.mul_slot);
@@ -1144,6 +1159,20 @@ int smx_comm_destroy(void* comm) {
     return nccl_err(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
 }
 
+int smx_comm_info(void* comm, int32_t* count, int32_t* rank, int32_t* device) {
+    if (!comm || !count || !rank || !device) return (int)hipErrorInvalidValue;
+    ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
+    int v = 0;
+    int err = nccl_err(ncclCommCount(c, &v));
+    if (err) return err;
+    *count = v;
+    if ((err = nccl_err(ncclCommUserRank(c, &v)))) return err;
+    *rank = v;
+    if ((err = nccl_err(ncclCommCuDevice(c, &v)))) return err;
+    *device = v;
+    return 0;
+}
+
 namespace {
 // Fused sharded chain, per pivot: k_pack<true> (step k's records -> header + candidate rows)
 // -> one ncclAllGather -> k_update<kShardFused> (merge, sweep, step k+1's records; with
@@ -1520,6 +1549,27 @@ int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t coun
     hipLaunchKernelGGL(k_fastdiv_bounded_check, dim3(1024), dim3(256), 0, S(stream), num, den,
                        count, out);
     return (int)hipGetLastError();
+}
+
+int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear) {
+#ifdef SMX_PATH_COUNT
+    if (!out || count < 0) return (int)hipErrorInvalidValue;
+    unsigned long long v[kPcCount];
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(v, HIP_SYMBOL(g_path_cnt), sizeof v);
+    if (e != hipSuccess) return (int)e;
+    for (int k = 0; k < count && k < kPcCount; ++k) out[k] = (int64_t)v[k];
+    if (clear) {
+        static const unsigned long long zero[kPcCount] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_path_cnt), zero, sizeof zero);
+    }
+    return e == hipSuccess ? kPcCount : (int)e;
+#else
+    (void)out;
+    (void)count;
+    (void)clear;
+    return -(int)hipErrorNotSupported;   // product build: no counters
+#endif
 }
 
 int smx_tune_block_form(int32_t form) {
@@ -2014,8 +2064,17 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                 errs[(size_t)q] = e;
             });
         for (auto& t : th) t.join();
+        int first = 0;
         for (int e : errs)
-            if (e) return e;
+            if (e && !first) first = e;
+        if (first) {
+            // a rank that failed mid-chain leaves the others' enqueued collectives waiting for
+            // it forever: abort every communicator (the caller must not destroy them afterwards,
+            // SMX_ERR_COMMS_ABORTED)
+            for (int q = 0; q < nranks; ++q)
+                (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(ranks[q].comm));
+            return SMX_ERR_COMMS_ABORTED;
+        }
         return 0;
     }
     return mshard_enqueue(ranks, nranks, parity, k, pivots, exchange);

@@ -13,7 +13,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsmx.so")
+# SMX_LIB names another build of the same library in this directory (tools: "libsmx_diag.so",
+# the sweep path counters of `make -C csrc diag`); the product loads libsmx.so
+LIB_PATH = os.path.join(HERE, os.path.basename(os.environ.get("SMX_LIB", "libsmx.so")))
 
 # outcome codes, include/smx.h
 PIVOT, OPTIMUM, INCORRECT, NOT_CONVERGE, FSHORT, IDLE = 0, 1, 2, 3, 4, 5
@@ -51,6 +53,7 @@ class Rank(ctypes.Structure):
 
 
 XCHG_RCCL, XCHG_COPY = 0, 1
+ERR_COMMS_ABORTED = -2000   # smx_mshard_run: a rank failed, every communicator was aborted
 
 _lib = None
 
@@ -74,6 +77,7 @@ EXPORTS = (
     "smx_bshard_pick", "smx_bshard_step_light", "smx_tune_shard_xchg",
     "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
     "smx_mshard_comms", "smx_mshard_run", "smx_int_first_fix", "smx_host_int_first_fix",
+    "smx_diag_path_counts", "smx_comm_info",
 )
 
 
@@ -145,6 +149,8 @@ def load():
                              ctypes.c_int),
         "smx_fastdiv_check": ([vp, vp, i64, vp, vp], ctypes.c_int),
         "smx_fastdiv_check_bounded": ([vp, vp, i64, vp, vp], ctypes.c_int),
+        "smx_diag_path_counts": ([ctypes.POINTER(i64), i32, i32], ctypes.c_int),
+        "smx_comm_info": ([vp] + [ctypes.POINTER(i32)] * 3, ctypes.c_int),
         "smx_tune_block": ([i32], ctypes.c_int),
         "smx_tune_block_pipe": ([i32], ctypes.c_int),
         "smx_tune_block_form": ([i32], ctypes.c_int),
@@ -287,6 +293,9 @@ def check(err: int, what: str) -> None:
     """Raise on a libsmx error: hipError_t codes, or -1000 - ncclResult_t for RCCL failures."""
     if err == 0:
         return
+    if err == ERR_COMMS_ABORTED:
+        raise RuntimeError(f"{what} failed: a rank could not enqueue its chain; every RCCL "
+                           "communicator was aborted")
     if err <= -1000:
         code = -1000 - err
         raise RuntimeError(f"{what} failed: RCCL {NCCL_RESULTS.get(code, code)}")

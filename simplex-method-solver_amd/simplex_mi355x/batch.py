@@ -34,7 +34,23 @@ def _eligible(cons, func) -> bool:
     if any(len(r) != m + 1 for r in cons):
         return False
     flen = len(func)
-    return flen in (m, m + 1) and flen >= 2
+    # int entries: the reference's first pivot runs in int arithmetic, whose zero signs differ
+    # from fp64's (engine._int_entries); SimplexMethod applies that fix, k_batch does not
+    return flen in (m, m + 1) and flen >= 2 and not _has_ints(cons, func)
+
+
+def _has_ints(cons, func) -> bool:
+    """Any entry an int (Python int / bool, numpy integer scalar or integer row), as
+    engine._int_entries counts them."""
+    for row in (*cons, func):
+        if isinstance(row, np.ndarray):
+            if row.dtype.kind in "iub":
+                return True
+            continue
+        for x in row:
+            if type(x) is not float and isinstance(x, (int, np.integer)):
+                return True
+    return False
 
 
 def _labels(n, m):

@@ -530,7 +530,11 @@ class SimplexMethod:
         start = self.pivots
         status = None
         while self.pivots - start < budget:
-            k = int(min(chunk, budget - (self.pivots - start), dev.log_cap))
+            # chunks end on multiples of `chunk` from the history's base, where hist.checkpoint
+            # keeps a table: after an int table's lone first pivot the next chunk is one shorter,
+            # so the later checkpoints are taken (else every replay starts at step 0)
+            k = chunk - (self.pivots - start) % chunk
+            k = int(min(k, budget - (self.pivots - start), dev.log_cap))
             if self._int0 is not None and self._pristine:
                 k = 1                      # the first pivot of an int table runs alone
             before = dev.step

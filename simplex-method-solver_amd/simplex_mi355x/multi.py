@@ -121,9 +121,12 @@ class MultiTableau:
         return arr
 
     def _native(self, k: int, pivots: int) -> None:
-        _lib.check(_lib.load().smx_mshard_run(
+        err = _lib.load().smx_mshard_run(
             self._structs, self.world, self.step & 1, int(k), int(pivots),
-            _lib.XCHG_RCCL if self.exchange == "rccl" else _lib.XCHG_COPY), "smx_mshard_run")
+            _lib.XCHG_RCCL if self.exchange == "rccl" else _lib.XCHG_COPY)
+        if err == _lib.ERR_COMMS_ABORTED:
+            self._comms = None   # aborted by the library: nothing left to destroy
+        _lib.check(err, "smx_mshard_run")
 
     def _sync(self) -> None:
         for dev in self.devices:

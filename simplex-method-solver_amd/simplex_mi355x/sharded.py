@@ -24,6 +24,7 @@ import contextlib
 import ctypes
 import json
 import os
+import socket
 import time
 
 import numpy as np
@@ -57,6 +58,13 @@ class RcclComm:
         h = ctypes.c_void_p()
         _lib.check(L.smx_comm_init(ctypes.byref(h), self.world, uid, self.rank), "smx_comm_init")
         self.handle = h.value
+
+    def info(self) -> tuple[int, int, int]:
+        """(ncclCommCount, ncclCommUserRank, ncclCommCuDevice) of this communicator."""
+        cnt, rk, dv = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(_lib.load().smx_comm_info(self.handle, ctypes.byref(cnt), ctypes.byref(rk),
+                                             ctypes.byref(dv)), "smx_comm_info")
+        return cnt.value, rk.value, dv.value
 
     def close(self):
         if self.handle:
@@ -505,6 +513,48 @@ def _enqueue_probe(be: BlockShardBackend, comm: "RcclComm", k: int, reps: int = 
 
 # ---------------------------------------------------------------------------------------------
 # bench.py --gpus N (launched by torch.distributed.run, one rank per GPU)
+def comm_record(comm, device_index: int, group=None) -> dict:
+    """What RCCL actually formed, from every rank (gathered; collective over `group`):
+    ``rccl_ranks`` = rank 0's ncclCommCount, and per rank its torch rank, ncclCommUserRank,
+    ncclCommCount, ncclCommCuDevice and the HIP device it runs on.  ``consistent``: every rank
+    sees the same count, equal to the torch world size, the user ranks are a permutation of
+    0..N-1 and no two ranks share a device."""
+    count, user_rank, comm_dev = comm.info()
+    mine = {"rank": dist.get_rank(group), "comm_count": int(count),
+            "comm_user_rank": int(user_rank), "comm_device": int(comm_dev),
+            "hip_device": int(device_index), "host": socket.gethostname()}
+    world = dist.get_world_size(group)
+    allr = [None] * world
+    dist.all_gather_object(allr, mine, group=group)
+    ok = (all(r["comm_count"] == world for r in allr)
+          and sorted(r["comm_user_rank"] for r in allr) == list(range(world))
+          and len({(r["host"], r["comm_device"]) for r in allr}) == world)
+    return {"rccl_ranks": allr[0]["comm_count"], "consistent": bool(ok), "ranks": allr}
+
+
+def sharded_cpu_baseline(cpu_baseline_fn, args, n: int, m: int, lo: int, hi: int,
+                         full_limit_bytes: int = 4 << 30):
+    """cpu_baseline of the multi-GPU line (rank 0, after the timed region): the CPU restatement
+    on the FULL tableau when it fits ``full_limit_bytes`` (16384^2: 2 GiB), else on rank 0's own
+    row block plus the f-row as an LP of its own (65536 x 32768: 17 GB); ``scope`` says which."""
+    R, C = n + 1, m + 1
+    seconds = float(getattr(args, "cpu_seconds", 15.0))
+    if 8 * R * C <= full_limit_bytes:
+        T = lp.dense_tableau(args.kind, args.seed, n, m)
+        out = cpu_baseline_fn(T, n, m, seconds)
+        out["scope"] = f"full {R}x{C} tableau (the same LP every rank holds a row block of)"
+    else:
+        nloc = hi - lo
+        T = np.zeros((nloc + 1, C), dtype=np.float64)
+        T[:-1] = lp.dense_rows(args.kind, args.seed, n, m, lo, hi)
+        T[-1, :m] = lp.objective(args.kind, args.seed, m)
+        out = cpu_baseline_fn(T, nloc, m, seconds)
+        out["scope"] = (f"rank 0's row block (rows {lo}..{hi - 1} + the f-row, {nloc + 1}x{C}) as "
+                        f"an LP of its own: the full {R}x{C} tableau is "
+                        f"{8 * R * C / 2**30:.1f} GiB")
+    return out
+
+
 def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
     for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"),
                  ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")):
@@ -581,6 +631,7 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
             enqueue = _enqueue_probe(be, comm, args.steps)
         except Exception as exc:   # noqa: BLE001 -- reported, not raised
             enqueue = {"error": f"{type(exc).__name__}: {exc}"}
+    rccl = comm_record(comm, device.index)
     local_bytes = 16.0 * (hi - lo + 1) * C
     ld = be.dev.ld
     # bytes each rank receives per pivot: full = every rank's slot (8 + 2 ld doubles); light =
@@ -635,8 +686,12 @@ def bench_main(args, metric, peak_gbs, cpu_baseline_fn=None, load_traffic=None):
             "trajectory_valid": bool(mn[2] > 0.5),
             "basis_cycle": cycle,
             "host_enqueue": enqueue,
+            "rccl_ranks": rccl["rccl_ranks"],
+            "rccl": rccl,
             "cpu_baseline": None,
         }
+        if cpu_baseline_fn is not None and not getattr(args, "no_cpu_baseline", False):
+            out["cpu_baseline"] = sharded_cpu_baseline(cpu_baseline_fn, args, n, m, lo, hi)
         print(json.dumps(out), flush=True)
     dist.barrier()
     if block:

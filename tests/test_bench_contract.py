@@ -110,7 +110,11 @@ def test_valu_table_matches_counter_summaries():
         # ~3 f64 ops per element-pivot (a FMA-shaped update plus the exact rounding fix-ups) and
         # the loads/stores/index arithmetic around them
         assert 6.0 < rec["instr_per_element_pivot"] < 12.0
-        assert rec["f64_fma_mul_add_share"] > 0.6
+        # the merged multi-pass summaries know the fp64 share; a single SQ_INSTS_VALU pass not
+        if "f64_fma_mul_add_share" in rec:
+            assert rec["f64_fma_mul_add_share"] > 0.6
+        else:
+            assert rec["source"].endswith(")") and "_counter_collection.csv" in rec["source"]
 
 
 def test_two_term_arithmetic(monkeypatch):

@@ -28,17 +28,17 @@ def test_batch_examples_full_solution():
     results, statuses = solve_batch(probs, max_pivots=50)
     for name, got in zip(names, results):
         exp = ex[name]["solution"]
-        cons = probs[names.index(name)][0]
-        ints = any(isinstance(x, int) for r in cons for x in r)
+        # int inputs (the demo LP) go through SimplexMethod, which reproduces the reference's
+        # int first pivot: zero signs included
         assert len(got) == len(exp), name
         for g, e in zip(got, exp):
             if e["kind"] == "error":
                 assert isinstance(g, simplex.Error) and str(g) == e["message"]
                 continue
             assert (g.row, g.column, g.i, g.j) == (e["row"], e["column"], e["i"], e["j"])
-            assert same_table(g.table, dec_table(e["table"]), signed_zero=not ints), name
+            assert same_table(g.table, dec_table(e["table"]), signed_zero=True), name
             for key in ("x1", "x2", "optimum"):
-                assert same_value(getattr(g, key), dec(e[key]), signed_zero=not ints)
+                assert same_value(getattr(g, key), dec(e[key]), signed_zero=True)
 
 
 def test_batch_every_trajectory_fixture():
@@ -123,3 +123,27 @@ def test_batch_no_history_matches_solve():
         assert same_table(got[1].table, exp[1].table)
         assert same_value(got[1].optimum, exp[1].optimum)
         assert got[1].row == exp[1].row and got[1].column == exp[1].column
+
+
+def test_batch_int_inputs_signed_zeros():
+    """Int and mixed int / float LPs (tests/golden/intzero.json, made by importing the reference):
+    solve_batch returns exactly SimplexMethod's get_solution, signed zeros of the int first pivot
+    included (such problems leave the batch kernel for SimplexMethod)."""
+    from simplex_mi355x.batch import solve_batch
+    import simplex
+    cases = [c for c in load("intzero.json")
+             if c["kind"] != "int_large" and c["outcome"]["kind"] != "cap"][::2]
+    probs = [dec_input(c["input"]) for c in cases]
+    results, statuses = solve_batch(probs, max_pivots=64)
+    checked = 0
+    for case, got in zip(cases, results):
+        steps = case["steps"]
+        infos = [g for g in got if not isinstance(g, simplex.Error)]
+        assert len(infos) == len(steps)
+        if case["outcome"]["kind"] == "error":
+            assert str(got[-1]) == case["outcome"]["message"]
+        for g, e in zip(infos, steps):
+            assert (g.i, g.j) == (e.get("i"), e.get("j"))
+            assert same_table(g.table, dec_table(e["table"]), signed_zero=True)
+        checked += 1
+    assert checked > 20

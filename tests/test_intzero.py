@@ -129,7 +129,11 @@ def test_gpu_get_solution_lazy(k):
     case = CASES[k]
     cons, func = dec_input(case["input"])
     sm = simplex.SimplexMethod([list(r) for r in cons], list(func), device="cuda:0")
-    _check_solution(sm.get_solution(max_pivots=_cap(case), lazy=True, chunk=4), case, simplex)
+    got = sm.get_solution(max_pivots=_cap(case), lazy=True, chunk=4)
+    # the chunks realign after the lone first pivot: a checkpoint every 4 pivots, not only at 0
+    hist = got[0]._history
+    assert sorted(hist.ckpt) == [s for s in range(0, sm.pivots + 1, 4)], sorted(hist.ckpt)
+    _check_solution(got, case, simplex)
 
 
 @pytest.mark.gpu

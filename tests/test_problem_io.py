@@ -70,3 +70,18 @@ def test_from_file_txt_host_engine_vs_reference_examples(tmp_path, name):
     import simplex
     from golden_util import check_txt_example
     check_txt_example(simplex.SimplexMethod, tmp_path, name, device="cpu")
+
+
+def test_batch_eligibility_excludes_int_inputs():
+    """solve_batch sends int / mixed problems to SimplexMethod (the int first-pivot fix), floats
+    to the batch kernel (CPU: eligibility only)."""
+    import numpy as np
+    from simplex_mi355x.batch import _eligible
+    fl = [[1.0, 1.0, -2.0], [-1.0, 1.0, 1.5], [1.0, -2.0, 4.0]]
+    assert _eligible(fl, [-1.0, -1.0])
+    assert not _eligible([[1, 1, -2], [-1, 1, 1.5], [1, -2, 4]], [-1, -1])
+    assert not _eligible(fl, [-1, -1.0])
+    assert not _eligible(fl[:2] + [[1.0, True, 4.0]], [-1.0, -1.0])
+    assert not _eligible([np.array([1, 1, -2])] + fl[1:], [-1.0, -1.0])
+    assert _eligible([np.array([1.0, 1.0, -2.0])] + fl[1:], [np.float64(-1.0), -1.0])
+    assert not _eligible(fl, [np.int32(-1), -1.0])
