@@ -6,12 +6,15 @@ the origin so the trajectory is a long phase-2 run), resident in HBM before timi
 A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): its selection
 (pick_element, :70-141) and its Jordan step over every element (recalculate_matrix, :143-177).
 At N = 1 on this table the steps run as block pivots: up to P pivots (the library's policy,
-smx_tune_block: 12 for tables of 256 MiB and more) are decided by one planner launch each
-(k_blk_step, every value of the intermediate tables re-derived from the block's input with the
-update's own expression) and applied by ONE sweep of the tableau (k_blk_sweep), so a sweep moves
-16 B per element for P pivots (a chain of k pivots is cut into blocks of near-equal size: 20
-pivots are two sweeps of 10); bit-identical to one pivot per sweep.  The one-pivot chain
-(k_update<kFused>, one kernel per pivot) is timed beside it as "single_pivot_update".
+smx_tune_block: 20 for tables of 1-4 GiB such as this one's 2 GiB, 12 from 256 MiB and beyond
+4 GiB, 10 from 48 MiB) are decided by one planner launch each (k_blk_step, every value of the
+intermediate tables re-derived from the block's input with the update's own expression) and
+applied by ONE sweep of the tableau (k_blk_sweep), so a sweep moves 16 B per element for P pivots
+(a chain of k pivots is cut into blocks of near-equal size: the driver's 20 pivots are ONE sweep
+of 20, the default 200 ten); bit-identical to one pivot per sweep.  After the timed region the
+line adds `sustained` (the next 200 pivots, HIP events around every sweep: the steady-state rate
+beside the burst) and times the one-pivot chain (k_update<kFused>, one kernel per pivot) as
+"single_pivot_update".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--size S]
 
@@ -377,7 +380,9 @@ def run_single(args):
         if instr is not None:
             extra["two_term"] = two_term(R, C, args.steps / len(sw), instr, avg_kernel,
                                          bytes_per_sweep)
-        kernels_per_pivot = (args.steps + len(sw)) / args.steps
+        # every launch of the chain: k_blk_prime + k_blk_first, per block Pb k_blk_step and
+        # k_blk_sweep + k_blk_sweep_rest, k_blk_publish
+        kernels_per_pivot = (args.steps + 2 * len(sw) + 3) / args.steps
     else:
         # the timed region replays one pre-captured hipGraph of K chained pivots (one fused
         # k_update per pivot, or the LDS-resident loop for tableaux that fit on chip); HIP events
@@ -406,7 +411,8 @@ def run_single(args):
             kernels_per_pivot = 1.0 / args.steps
         else:
             kernel = "k_update<kFused>" if _lib.fused_enabled() else "k_update<kSingle>"
-            kernels_per_pivot = 1 if _lib.fused_enabled() else 2
+            # fused: k_la_prime, K k_update, k_publish; unfused: k_select + k_update per pivot
+            kernels_per_pivot = (args.steps + 2) / args.steps if _lib.fused_enabled() else 2
             extra = {"pivots_per_launch": 1}
         traffic = load_traffic(args.traffic, f"{R}x{C}")
     ctl = dev.sync_state()
