@@ -102,6 +102,9 @@ def parse():
                     help="row-sharded block path: exchange per pivot (full = all-gather of every "
                          "rank's header + 2 candidate rows; light = header all-gather + one "
                          "max all-reduce of the pivot row; auto = light from 4 ranks on)")
+    ap.add_argument("--block-pivots", type=int, default=0,
+                    help="N = 1: pivots per sweep (smx_tune_block; 0 = the library's policy, "
+                         "20 at 16384^2)")
     ap.add_argument("--sustained", type=int, default=200,
                     help="block path, N = 1: after the timed region, time this many further "
                          "pivots with HIP events around every sweep (the steady-state rate beside "
@@ -340,6 +343,8 @@ def run_single(args):
 
     n, m = shape_of(args)
     R, C = n + 1, m + 1
+    if args.block_pivots:
+        _lib.tune_block(args.block_pivots)
     T = lp.dense_tableau(args.kind, args.seed, n, m)
     dev = DeviceTableau(T, n, m, m, device="cuda:0", log_cap=max(1 << 16, args.warmup + args.steps))
     if args.warmup:

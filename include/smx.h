@@ -327,7 +327,10 @@ int smx_fastdiv_check_bounded(const double* num, const double* den, int64_t coun
 /* Diagnostic: the block sweep's units (one row x 128 columns) per path, summed over every
  * k_blk_sweep launch since the last clear -- out[0..count) = fast, zero-extended, window-tracked,
  * window vote failed (-> exact), exact directly, units in chunks not free / not zero-safe, units of
- * rows flagged 0 / 3, inputs out of bounds on a free chunk and flag-1 row (smx_block.hpp kPc*).
+ * rows flagged 0 / 3, inputs out of bounds on a free chunk and flag-1 row, units in chunks whose
+ * pivots / pivot-row values fail the bounds, then per wave the shader clock (s_memtime) and the
+ * 100 MHz real time (s_memrealtime) over its sweep body -- their ratio is the clock the sweep
+ * ran at (smx_block.hpp kPc*).
  * Synchronises the device.  Returns the number of counters, or -hipErrorNotSupported in the
  * product build (the counters exist only in libsmx_diag.so, `make -C csrc diag`). */
 int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear);

@@ -220,7 +220,17 @@ __device__ __forceinline__ bool bnd_or_zero(double v) {
 __device__ __forceinline__ double fd_zero(double n, double e, double y) {
     const double t = n * y;
     const double r = fma(-e, t, n);
-    return __builtin_amdgcn_div_fixup(fma(r, y, t), e, n);
+    const double q = fma(r, y, t);
+#ifdef SMX_FDZERO_FIXUP
+    return __builtin_amdgcn_div_fixup(q, e, n);
+#else
+    // The same result without v_div_fixup_f64 (several issue slots on gfx950: the zero-extended
+    // path ran ~1.7x the fast path's time per unit, profiles/r05a/): a zero numerator gives a
+    // zero q (r = +0 then) whose only wrong bit can be the sign, and t = n y is that zero with
+    // the right sign, sign(n) xor sign(e) -- so the high dword comes from t there.
+    const int hi = (n == 0.0) ? __double2hiint(t) : __double2hiint(q);
+    return __hiloint2double(hi, __double2loint(q));
+#endif
 }
 
 // Self-check of the unchecked sequences on the domains the bounds guarantee (smx_fastdiv_check
@@ -1348,16 +1358,25 @@ enum : int {
     kPcRowFlag0,        // units of rows with flag 0 (a multiplier unbounded, not zero)
     kPcRowFlag3,        // units of rows with flag 3 (bounded or zero, at least one zero)
     kPcXFail,           // chunk_free and flag 1, but an input element out of bounds
+    kPcChunkE,          // units in chunks whose pivots fail (e outside the window / bounds)
+    kPcChunkP,          // units in chunks with a pivot-row value neither bounded nor zero
+    kPcClkCycles,       // per wave: s_memtime ticks (shader clock) over the wave's sweep body
+    kPcClkTicks,        // per wave: s_memrealtime ticks (100 MHz) over the same span
     kPcCount
 };
 #ifdef SMX_PATH_COUNT
 __device__ unsigned long long g_path_cnt[kPcCount];
-#define SMX_PC_DECL uint32_t pc_cnt[kPcCount] = {};
+#define SMX_PC_DECL                                                                             \
+    uint64_t pc_cnt[kPcCount] = {};                                                             \
+    const uint64_t pc_t0 = __builtin_amdgcn_s_memtime();                                        \
+    const uint64_t pc_r0 = __builtin_amdgcn_s_memrealtime();
 #define SMX_PC(k) (++pc_cnt[(k)])
 #define SMX_PC_FLUSH                                                                            \
     do {                                                                                        \
+        pc_cnt[kPcClkCycles] = __builtin_amdgcn_s_memtime() - pc_t0;                            \
+        pc_cnt[kPcClkTicks] = __builtin_amdgcn_s_memrealtime() - pc_r0;                         \
         const int l_ = threadIdx.x & (kWave - 1);                                               \
-        uint32_t v_ = 0;                                                                        \
+        uint64_t v_ = 0;                                                                        \
         _Pragma("unroll") for (int k_ = 0; k_ < kPcCount; ++k_) if (l_ == k_) v_ = pc_cnt[k_];  \
         if (l_ < kPcCount && v_) atomicAdd(&g_path_cnt[l_], (unsigned long long)v_);            \
     } while (0)
@@ -1476,6 +1495,8 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
 #ifdef SMX_PATH_COUNT
         if (!chunk_free) SMX_PC(kPcChunkNotFree);
         if (!chunk_zok) SMX_PC(kPcChunkNotZok);
+        if (!(allok && et < kBndSpan)) SMX_PC(kPcChunkE);
+        if (!__all(zok)) SMX_PC(kPcChunkP);
         if (rf == 0) SMX_PC(kPcRowFlag0);
         if (rf == 3) SMX_PC(kPcRowFlag3);
         if (chunk_free && rf == 1 && !__all(xt < kBndXMax)) SMX_PC(kPcXFail);

@@ -640,12 +640,12 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
         if (((int64_t)grid * kUpdWaves) % nchunks != 0) form = 5;
     }
     BlkSweepFn fn = blk_sweep_fn(P, form);
-    if (form == 5)   // as many workgroups per CU as are resident (at most 8): the P KiB of
-                     // pivot-row slices in LDS and ~106 SGPRs cap it at 7 from P = 16 (6 at 24);
-                     // a grid sized for 8 left 1/8 of the rows to a second residency round.
-                     // smx_tune_set(-2, bpc) overrides it (A/B timing)
-        grid = sweep_grid_lds(s, g_blocks_per_cu > 0 ? g_blocks_per_cu
-                                                     : resident_bpc((const void*)fn, 8));
+    if (form == 5)   // a grid of 8 workgroups per CU.  At P = 20 only 7 are resident (P KiB of
+                     // pivot-row slices in LDS, ~106 SGPRs), but the sweep is fp64-issue-bound
+                     // there and the grid sized for 8 is as fast as 7 and faster than the
+                     // occupancy API's 6: 16384^2, 200 pivots, mean sweep 1.464 / 1.488 / 1.503 ms
+                     // at 8 / 7 / 6 (profiles/r05a/).  smx_tune_set(-2, bpc) overrides it.
+        grid = sweep_grid_lds(s, g_blocks_per_cu > 0 ? g_blocks_per_cu : 8);
     BlkHdr* hs = reinterpret_cast<BlkHdr*>(blk);
     const BlkHdr* h = reinterpret_cast<const BlkHdr*>(blk + kBlkHdrBytes * slot);
     const double* mul = reinterpret_cast<const double*>(blk + L.mul + slot * L.mul_slot);

@@ -22,7 +22,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "simplex-method-solver_amd")]
 
 PATHS = ["fast", "zero", "window", "window_fail", "exact", "chunk_not_free", "chunk_not_zok",
-         "row_flag0", "row_flag3", "x_fail"]
+         "row_flag0", "row_flag3", "x_fail", "chunk_e", "chunk_p", "clk_cycles", "clk_ticks"]
 
 
 def main() -> None:
@@ -82,7 +82,9 @@ def main() -> None:
             tot_counts += c
             units = int(c[0] + c[1] + c[2] + c[3] + c[4])
             rec["units"] = units
-            rec["paths"] = {k: int(v) for k, v in zip(PATHS, c) if v}
+            rec["paths"] = {k: int(v) for k, v in zip(PATHS[:12], c[:12]) if v}
+            if c[13]:   # shader clock over the sweep bodies (s_memtime / s_memrealtime at 100 MHz)
+                rec["clock_ghz"] = round(float(c[12]) / float(c[13]) * 0.1, 4)
         sweeps.append(rec)
         print(json.dumps(rec), flush=True)
         done += P
@@ -97,8 +99,11 @@ def main() -> None:
     if diag:
         units = int(tot_counts[:5].sum())
         summ["units"] = units
-        summ["path_share"] = {k: round(int(v) / units, 5) for k, v in zip(PATHS, tot_counts)
+        summ["path_share"] = {k: round(int(v) / units, 5) for k, v in zip(PATHS[:12],
+                                                                          tot_counts[:12])
                               if v and units}
+        if tot_counts[13]:
+            summ["clock_ghz"] = round(float(tot_counts[12]) / float(tot_counts[13]) * 0.1, 4)
     print(json.dumps(summ), flush=True)
 
 
