@@ -485,6 +485,13 @@ typedef struct smx_rank {
 int smx_mshard_comms(void** comms_out, int32_t nranks, const int32_t* devices);
 int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
                    int32_t pivots, int32_t exchange);
+/* smx_mshard_run's k pivots with the copy exchange, every rank on ranks[0]'s device (the host-
+ * bound case: ~3N host calls per pivot), captured once as ONE graph on ranks[0].stream -- the
+ * other ranks' streams fork from and join back into it, and every event the capture records is
+ * its own, recorded exactly once.  Replay with smx_graph_launch(graph, ranks[0].stream), free
+ * with smx_graph_destroy.  Opt-in (SimplexMethod(..., devices=[d] * N) with graph_chain=True). */
+int smx_mshard_graph_create(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
+                            int32_t pivots, void** graph_out);
 /* ---- Host engine (no device): the same pick_element / recalculate_matrix on a HOST tableau --
  * For machines without an MI355X (the reference UI's 2-variable LPs, BASELINE.json configs[0]).
  * Pointers here are HOST pointers (same layout as the device tableau: row-major fp64, R = n + 1

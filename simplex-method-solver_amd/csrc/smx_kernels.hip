@@ -1894,8 +1894,13 @@ bool mshard_args_ok(const smx_rank* ranks, int32_t nranks, int32_t k, int32_t pi
 // Every launch of k chained pivots on every rank, enqueued from this thread (smx_mshard_run)
 // ev_ext: the copy exchange's 2 * nranks events created by the caller, or NULL: created and
 // destroyed here.
+// pool (graph capture, one-device copy exchange only): every event record of the exchange takes
+// a fresh event from it, never re-recording one inside the capture (round 4's capture re-recorded
+// each rank's events once per pivot and crashed the host process in smx_mshard_graph_create,
+// gpurun_out r04g / r04h); `pool_n` events, created by the caller on ranks[0]'s device.
 int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
-                   int32_t pivots, int32_t exchange, hipEvent_t* ev_ext = nullptr) {
+                   int32_t pivots, int32_t exchange, hipEvent_t* ev_ext = nullptr,
+                   hipEvent_t* pool = nullptr, int pool_n = 0) {
     int dev0 = 0;
     (void)hipGetDevice(&dev0);
     const size_t slot = (size_t)SMX_SHARD_HDR + 2 * (size_t)ranks[0].shape.ld;
@@ -1974,9 +1979,19 @@ int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                 // one launch, and every other rank waits for that launch: 3N - 1 host calls per
                 // pivot.  A rank's next pack follows its wait, so no slot is overwritten early.
                 hipStream_t st0 = on(0);
+                auto pick = [&](hipEvent_t own) -> hipEvent_t {   // fresh event when capturing
+                    if (!pool) return own;
+                    if (pool_n <= 0) {
+                        err = (int)hipErrorInvalidValue;
+                        return own;
+                    }
+                    --pool_n;
+                    return *pool++;
+                };
                 for (int q = 1; q < nranks && !err; ++q) {
-                    err = (int)hipEventRecord(ev[2 * q], on(q));
-                    if (!err) err = (int)hipStreamWaitEvent(st0, ev[2 * q], 0);
+                    const hipEvent_t e = pick(ev[2 * q]);
+                    if (!err) err = (int)hipEventRecord(e, on(q));
+                    if (!err) err = (int)hipStreamWaitEvent(st0, e, 0);
                 }
                 const int gx = (int)((slot + 256 * 8 - 1) / (256 * 8));
                 if (!err) {
@@ -1985,9 +2000,10 @@ int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                                        st0, ms, nranks, (int64_t)slot);
                     err = (int)hipGetLastError();
                 }
-                if (!err) err = (int)hipEventRecord(ev[1], st0);
+                const hipEvent_t eg = err ? ev[1] : pick(ev[1]);
+                if (!err) err = (int)hipEventRecord(eg, st0);
                 for (int q = 1; q < nranks && !err; ++q)
-                    err = (int)hipStreamWaitEvent(on(q), ev[1], 0);
+                    err = (int)hipStreamWaitEvent(on(q), eg, 0);
             } else {   // every rank copies every send slot into its recv, ordered by events
                 for (int q = 0; q < nranks && !err; ++q)
                     err = (int)hipEventRecord(ev[2 * q], on(q));
@@ -2078,6 +2094,56 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
         return 0;
     }
     return mshard_enqueue(ranks, nranks, parity, k, pivots, exchange);
+}
+
+int smx_mshard_graph_create(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
+                            int32_t pivots, void** graph_out) {
+    if (!mshard_args_ok(ranks, nranks, k, pivots, SMX_XCHG_COPY) || k < 1 || !graph_out ||
+        nranks > kMsMaxRanks)
+        return (int)hipErrorInvalidValue;
+    for (int q = 1; q < nranks; ++q)
+        if (ranks[q].device != ranks[0].device) return (int)hipErrorInvalidValue;
+    int dev0 = 0;
+    (void)hipGetDevice(&dev0);
+    hipStream_t st0 = S(ranks[0].stream);
+    // every event the capture records, created before it and destroyed after it, each recorded
+    // exactly once: [0] the fork, [1 .. nranks) the joins, then nranks per pivot (the exchange)
+    const int pool_n = nranks * k;
+    const int nev = nranks + pool_n;
+    std::vector<hipEvent_t> ev((size_t)nev, nullptr);
+    std::vector<hipEvent_t> xev(2 * (size_t)nranks, nullptr);   // unused in pool mode
+    int err = (int)hipSetDevice(ranks[0].device);
+    for (int q = 0; q < nev && !err; ++q)
+        err = (int)hipEventCreateWithFlags(&ev[(size_t)q], hipEventDisableTiming);
+    Graph* g = new Graph();
+    if (!err) err = (int)hipStreamBeginCapture(st0, hipStreamCaptureModeThreadLocal);
+    if (!err) {
+        int lerr = (int)hipEventRecord(ev[0], st0);   // fork: every rank's stream joins
+        for (int q = 1; q < nranks && !lerr; ++q)
+            lerr = (int)hipStreamWaitEvent(S(ranks[q].stream), ev[0], 0);
+        if (!lerr)
+            lerr = mshard_enqueue(ranks, nranks, parity, k, pivots, SMX_XCHG_COPY, xev.data(),
+                                  ev.data() + nranks, pool_n);
+        for (int q = 1; q < nranks && !lerr; ++q) {   // join back into ranks[0]'s stream
+            lerr = (int)hipEventRecord(ev[(size_t)q], S(ranks[q].stream));
+            if (!lerr) lerr = (int)hipStreamWaitEvent(st0, ev[(size_t)q], 0);
+        }
+        (void)hipSetDevice(ranks[0].device);
+        const hipError_t e2 = hipStreamEndCapture(st0, &g->graph);
+        err = lerr ? lerr : (int)e2;
+    }
+    if (!err) err = (int)hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    (void)hipSetDevice(dev0);
+    if (err) {
+        if (g->exec) (void)hipGraphExecDestroy(g->exec);
+        if (g->graph) (void)hipGraphDestroy(g->graph);
+        delete g;
+        return err;
+    }
+    *graph_out = g;
+    return 0;
 }
 
 int smx_int_first_fix(const double* T0, double* T1, int64_t ld, int32_t rows, int32_t cols,

@@ -77,7 +77,7 @@ EXPORTS = (
     "smx_bshard_pick", "smx_bshard_step_light", "smx_tune_shard_xchg",
     "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
     "smx_mshard_comms", "smx_mshard_run", "smx_int_first_fix", "smx_host_int_first_fix",
-    "smx_diag_path_counts", "smx_comm_info",
+    "smx_diag_path_counts", "smx_comm_info", "smx_mshard_graph_create",
 )
 
 
@@ -151,6 +151,8 @@ def load():
         "smx_fastdiv_check_bounded": ([vp, vp, i64, vp, vp], ctypes.c_int),
         "smx_diag_path_counts": ([ctypes.POINTER(i64), i32, i32], ctypes.c_int),
         "smx_comm_info": ([vp] + [ctypes.POINTER(i32)] * 3, ctypes.c_int),
+        "smx_mshard_graph_create": ([ctypes.POINTER(Rank), i32, i32, i32, i32,
+                                     ctypes.POINTER(vp)], ctypes.c_int),
         "smx_tune_block": ([i32], ctypes.c_int),
         "smx_tune_block_pipe": ([i32], ctypes.c_int),
         "smx_tune_block_form": ([i32], ctypes.c_int),

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .device import int_first_fix
+from .device import Graph, int_first_fix
 from .sharded import BlockShardBackend, row_range
 
 
@@ -59,7 +59,8 @@ class MultiTableau:
     is_host = False
 
     def __init__(self, dense: np.ndarray, n: int, m: int, flen: int, devices, *,
-                 pivots: int | None = None, log_cap: int = 1 << 16, exchange: str | None = None):
+                 pivots: int | None = None, log_cap: int = 1 << 16, exchange: str | None = None,
+                 graph_chain: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("simplex_mi355x needs an MI355X (HIP device); there is no CPU path")
         L = _lib.load()
@@ -96,6 +97,12 @@ class MultiTableau:
             _lib.check(L.smx_mshard_comms(comms, P, devs), "smx_mshard_comms")
             self._comms = [comms[p] for p in range(P)]
         self._structs = self._rank_structs()
+        # opt-in: chained runs of ranks sharing ONE device (copy exchange) replay a captured graph
+        # per (parity, k) -- one host call per chain instead of ~3N per pivot
+        # (smx_mshard_graph_create); other layouts enqueue eagerly
+        self.graph_chain = bool(graph_chain) and self.exchange == "copy" and \
+            len({d.index for d in self.devices}) == 1 and P <= 16
+        self._graphs = {}
         self.step = 0
         self._term = False
         self._saved = None        # control blocks before a pick() not yet applied
@@ -120,7 +127,18 @@ class MultiTableau:
             a.shape = _lib.Shape(*d.shape)
         return arr
 
-    def _native(self, k: int, pivots: int) -> None:
+    def _native(self, k: int, pivots: int, graph: bool = False) -> None:
+        if graph and self.graph_chain:
+            key = (self.step & 1, int(k), int(pivots))
+            g = self._graphs.get(key)
+            if g is None:
+                h = ctypes.c_void_p()
+                _lib.check(_lib.load().smx_mshard_graph_create(
+                    self._structs, self.world, self.step & 1, int(k), int(pivots),
+                    ctypes.byref(h)), "smx_mshard_graph_create")
+                g = self._graphs[key] = Graph(h.value)
+            g.launch(self.ranks[0].dev.stream.cuda_stream)
+            return
         err = _lib.load().smx_mshard_run(
             self._structs, self.world, self.step & 1, int(k), int(pivots),
             _lib.XCHG_RCCL if self.exchange == "rccl" else _lib.XCHG_COPY)
@@ -317,7 +335,7 @@ class MultiTableau:
         self._restore()
         if self._term:
             self.clear_term()
-        self._native(k, self.P)
+        self._native(k, self.P, graph=graph)
         for be in self.ranks:
             be.dev.step += k
             be.dev._pending = True
@@ -339,6 +357,9 @@ class MultiTableau:
         self._term = False
 
     def close(self) -> None:
+        for g in getattr(self, "_graphs", {}).values():
+            g.destroy()
+        self._graphs = {}
         if self._comms:
             L = _lib.load()
             for h in self._comms:

@@ -200,3 +200,27 @@ def test_multi_rccl_exchange_world1_vs_oracle(light):
         sm._dev.close()
     finally:
         _lib.tune_shard_xchg(prev)
+
+
+@pytest.mark.parametrize("kind,n,m,world,k,chunk", [
+    ("uniform", 2047, 2047, 4, 48, 16),      # one captured graph, replayed three times
+    ("mixed", 1500, 900, 3, 36, 12),         # phase 1
+    ("degenerate", 1023, 1023, 8, 40, 20),
+])
+def test_multi_graph_chain_vs_oracle(kind, n, m, world, k, chunk):
+    """Ranks sharing one device with graph_chain (smx_mshard_graph_create: the chain captured
+    once, every event of the capture recorded exactly once): pivots and the whole table bit for
+    bit against the C oracle, the graph replayed for every chunk."""
+    import simplex
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    T = lp.dense_tableau(kind, 13, n, m)
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist(), devices=[0] * world)
+    sm._dev.graph_chain = True
+    sm.solve(record_history=False, max_pivots=k, chunk=chunk)
+    assert len(sm._dev._graphs) >= 1
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    D = sm._dev.download()
+    assert np.array_equal(D[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(D[n, :m].view(np.int64), Tref[n, :m].view(np.int64))

@@ -32,6 +32,9 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--exchange", default=None, help="copy (default on one device) or rccl "
                     "(one host thread per device; one rank per device, so world 1 here)")
+    ap.add_argument("--forms", default="eager,graph",
+                    help="eager (smx_mshard_run) and / or graph (smx_mshard_graph_create: copy "
+                         "exchange on one device, one replay per chain)")
     a = ap.parse_args()
     import torch
     from simplex_mi355x import lp
@@ -39,11 +42,13 @@ def main() -> None:
     n = m = a.size - 1
     T = lp.dense_tableau("uniform", 0, n, m)
     for world in (int(x) for x in a.ranks.split(",")):
-        mt = MultiTableau(T, n, m, m, ["cuda:0"] * world, pivots=a.pivots, exchange=a.exchange)
+        mt = MultiTableau(T, n, m, m, ["cuda:0"] * world, pivots=a.pivots, exchange=a.exchange,
+                          graph_chain="graph" in a.forms)
         mt.run(a.pivots, graph=False)   # warm-up: prime, first kernels
         mt.sync_state()
         logs = {}
-        for graph in (False,):
+        forms = [f == "graph" for f in a.forms.split(",") if f == "eager" or mt.graph_chain]
+        for graph in forms:
             host, wall = [], []
             for rep in range(a.reps + (1 if graph else 0)):   # graph: the first run captures
                 mt.upload(T)
@@ -60,6 +65,8 @@ def main() -> None:
                 host.append((t1 - t0) / a.k * 1e6)
                 wall.append((t2 - t0) / a.k * 1e6)
             logs[graph] = mt.read_log(0, a.k).tolist()
+            if len(logs) == 2:   # the graph replays exactly the eager chain's pivots
+                assert logs[True] == logs[False]
             dev = min(wall)
             print(json.dumps({"size": a.size, "ranks": world, "exchange": mt.exchange,
                               "form": "graph" if graph else "eager",
