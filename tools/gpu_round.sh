@@ -3,7 +3,8 @@
 # limit, tools/gpu_steps.sh: a fault / abort / time-out ends the session there; a failing test does
 # not).  Replaces the round-4 one-off tools/gpu_r04*.sh scripts.
 #   usage (from the repo root, e.g. through gpurun):  tools/gpu_round.sh TAG RECIPE...
-# Output under gpurun_out/TAG/ (one <recipe>.log each, steps.log).  Recipes (ARGS: spaces as ','):
+# Output under gpurun_out/TAG/ (one <recipe>.log each, steps.log).  Recipes (ARGS: spaces as ',',
+# a literal comma as '+', e.g. `py=tools/mshard_host_cost.py,--ranks,1+2+4+8`):
 #   pytest                 the full `pytest -m gpu` suite (the driver's round-end tier)
 #   pytest=FILES           those test files (comma separated) with -m gpu
 #   smoke                  __graft_entry__.smoke()
@@ -38,6 +39,7 @@ for spec in "$@"; do
   arg=""
   [[ "$spec" == *=* ]] && arg="${spec#*=}"
   arg="${arg//,/ }"
+  arg="${arg//+/,}"
   tag="${n}_${name}"
   case "$name" in
     pytest)
