@@ -357,6 +357,11 @@ int smx_tune_block(int32_t pivots);
  * and wherever the register layout's grid cannot give every wave one column chunk), 4 registers,
  * 5 LDS; any other value keeps the setting.  Returns the previous one.  Same bits either way. */
 int smx_tune_block_form(int32_t form);
+/* Persistent planner (csrc/smx_plan.hpp): 1 = every block of an unsharded chain is planned by ONE
+ * launch (k_blk_plan: its workgroups stay resident for the block's P steps and hand each step's
+ * records to the next through tagged granules), 0 = one launch per pivot (k_blk_step); -1 queries.
+ * Same decisions and bits either way.  Returns the previous setting. */
+int smx_tune_block_persist(int32_t on);
 /* Pipelined block chains (default 0): with more than one block, block b+1 is planned on a second
  * stream of the library while block b is swept (from block b's input table, every chain prefixed
  * by block b's pivots), the sweeps work out of place, the ragged block comes first, and a final

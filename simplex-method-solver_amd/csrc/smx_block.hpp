@@ -90,6 +90,8 @@ struct BlkHdr {
     int32_t loc;                     // buffer index (0/1) of the newest table a sweep wrote
     double e[kBlkMax], y[kBlkMax];   // pivot element and its refined reciprocal (fd_prep)
     int64_t np0;                     // ctl->npivots when the chain started
+    uint32_t pepoch;                 // persistent planner (smx_plan.hpp): launches so far, the
+                                     // tag epoch of its record granules (slot 0 only)
 };
 constexpr int64_t kBlkHdrBytes = 1024;   // one plan slot's header
 static_assert(sizeof(BlkHdr) <= kBlkHdrBytes, "block header");
@@ -106,7 +108,7 @@ __host__ __device__ __forceinline__ int blk_slot(int l, int P, int bn) {
 // planner's column cache (blk_step_body).  The second header / mul / pr (plan slot 1) is used by
 // pipelined chains only.
 struct BlkLayout {
-    int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot;
+    int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, xr;
 };
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
@@ -121,7 +123,9 @@ inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     L.fr = L.pr + 2 * L.pr_slot;
     // then the planner's column caches: [R] "-b" column and [2][R] the next records' column of
     // T_k (pipelined form), [2][R] T_{k+L}[i][cf] and [2][R] T_{k+L}[i][m] (register form)
-    L.bytes = blk_align(L.fr + 2 * ld * 8 + 7 * R * 8);
+    // then the persistent planner's record granules: [2 step parities][kBlkPartsMax][8] uint64
+    L.xr = blk_align(L.fr + 2 * ld * 8 + 7 * R * 8);
+    L.bytes = blk_align(L.xr + (int64_t)2 * kBlkPartsMax * 8 * 8);
     return L;
 }
 
@@ -469,6 +473,39 @@ __device__ __forceinline__ void blk_rec_add(BlkRec& R, int i, double bv, bool ha
             if (better(x, R.bc)) R.bc = x;
         }
     }
+}
+
+// The workgroup's record (thread 0 holds it afterwards; the others an unspecified value)
+__device__ __forceinline__ smx_part blk_rec_reduce(BlkRec R) {
+    __shared__ int s_b[kBlkNT / kWave];
+    __shared__ First s_f[kBlkNT / kWave];
+    __shared__ Cand s_c[kBlkNT / kWave];
+    const int tid = threadIdx.x;
+    int nb = wave_min_int_dpp(R.nb);
+    First f = wave_first_dpp(R.f);
+    Cand bc = wave_best_dpp(R.bc);
+    const int wid = tid >> 6;
+    if ((tid & 63) == 0) {
+        s_b[wid] = nb;
+        s_f[wid] = f;
+        s_c[wid] = bc;
+    }
+    __syncthreads();
+    smx_part pt{};
+    if (tid == 0) {
+        for (int w = 1; w < kBlkNT / kWave; ++w) {
+            nb = min(nb, s_b[w]);
+            if (s_f[w].idx < f.idx) f = s_f[w];
+            if (better(s_c[w], bc)) bc = s_c[w];
+        }
+        pt.p1col = nb;
+        pt.first = f.idx;
+        pt.first_v = f.v;
+        pt.best_cls = bc.cls;
+        pt.best_i = bc.idx;
+        pt.best_v = bc.v;
+    }
+    return pt;
 }
 
 __device__ __forceinline__ void blk_rec_store(BlkRec R, smx_part* out) {

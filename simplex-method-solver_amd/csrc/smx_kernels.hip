@@ -52,6 +52,7 @@ static_assert(sizeof(smx_part) == 32, "smx_part layout");
 #include "smx_batch.hpp"
 #include "smx_resident.hpp"
 #include "smx_block.hpp"
+#include "smx_plan.hpp"
 #include "smx_host.hpp"
 #include "smx_intfirst.hpp"
 
@@ -457,10 +458,12 @@ constexpr int64_t kBlockWideTable = 256ll << 20;
 // k_blk_sweep<P, 5>): at 16384^2 the per-pivot cost is flat from 12 to 20 (99.4 / 101.5 / 99.1 us
 // at 12 / 16 / 20, profiles/r04r/; 100.8 / 98.4 / 97.8 on another box, profiles/r04e/), so the
 // larger bound only changes how a chain is cut -- 20 pivots become ONE sweep of 20 instead of two
-// of 10 (106.8 us per pivot at 10).  Beyond 4 GiB (config 5's 17 GB) and below 1 GiB (8192^2:
-// 32.0 / 33.6 / 36.1 us at 12 / 14 / 16, where the planner's share is larger) it stays at 12.
+// of 10 (106.8 us per pivot at 10); at 200 pivots 12 and 20 tie (10,426 / 10,455 pivots/s,
+// profiles/r05b/).  Round 5: also beyond 4 GiB -- config 5 (65536 x 32768 degenerate, 17 GB)
+// sweeps at 803 / 773 / 743 / 744 us per pivot with 12 / 16 / 20 / 24 pivots per sweep, planner
+// 26 / 30 us per pivot at 12 / 20 (profiles/r05b/).  Below 1 GiB (8192^2: 32.0 / 33.6 / 36.1 us
+// at 12 / 14 / 16, where the planner's share is larger) it stays at 12.
 constexpr int64_t kBlockHugeTable = 1ll << 30;
-constexpr int64_t kBlockHugeTableMax = 4ll << 30;
 
 int block_pivots(const smx_shape& s) {
     if (g_block == 1) return 0;
@@ -468,7 +471,7 @@ int block_pivots(const smx_shape& s) {
     if (g_block >= 2) return g_block;
     const int64_t bytes = (int64_t)(s.rows + 1) * s.ld * 8;
     if (bytes < kBlockMinTable) return 0;
-    if (bytes >= kBlockHugeTable && bytes < kBlockHugeTableMax) return 20;
+    if (bytes >= kBlockHugeTable) return 20;
     return bytes >= kBlockWideTable ? 12 : 10;
 }
 
@@ -518,6 +521,26 @@ BlkStepFn blk_step_fn_sh(int L) {
     using All = std::make_integer_sequence<int, kBlkMax>;
     if (LAG) return blk_lag_pick(L, All{});
     return blk_step_pick<SH>(L, All{});
+}
+
+using BlkPlanFn = void (*)(const double*, int64_t, int, int, int, int, int, int, smx_ctl*,
+                          BlkHdr*, smx_part*, double*, double*, double*, int32_t*, double*,
+                          int64_t, uint64_t*);
+template <int... Is>
+BlkPlanFn blk_plan_pick(int P, std::integer_sequence<int, Is...>) {
+    static const BlkPlanFn t[] = {k_blk_plan<Is + 1>...};
+    return t[P - 1];
+}
+
+// smx_tune_block_persist: 1 plans every block of an unsharded, unpipelined chain in ONE
+// persistent launch (k_blk_plan, smx_plan.hpp) where each thread owns at most one row; 0 one
+// launch per pivot (k_blk_step).
+int g_block_persist = 0;
+bool plan_persistent(const smx_shape& s) {
+    if (!g_block_persist) return false;
+    const int G = blk_parts_of(s.nparts, s.rows);
+    return s.row0 == 0 && s.rows == s.n && (int64_t)s.rows <= (int64_t)G * kBlkNT &&
+           G <= num_cus();
 }
 
 template <int... Is>
@@ -596,6 +619,18 @@ int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
     hipLaunchKernelGGL(bsh_pack_fn(D), dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
                        s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h[0], (const smx_part*)b.parts,
                        blk_parts_of(s.nparts, s.rows), (const double*)b.mul[0], (const double*)b.pr[0], send);
+    return (int)hipGetLastError();
+}
+
+// Block bn's P planner steps in one persistent launch (plan slot 0)
+int launch_blk_plan(const double* T, const smx_shape& s, int P, int parity, int bn, smx_ctl* ctl,
+                    const BlkPtrs& b, char* blk, int32_t* log, double* xhist, int64_t log_cap,
+                    hipStream_t st) {
+    const int G = blk_parts_of(s.nparts, s.rows);
+    hipLaunchKernelGGL(blk_plan_pick(P, std::make_integer_sequence<int, kBlkMax>{}), dim3(G),
+                       dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen, fscan_of(s), parity, bn,
+                       ctl, b.h[0], b.parts, b.mul[0], b.pr[0], b.fr, log, xhist, log_cap,
+                       reinterpret_cast<uint64_t*>(blk + b.L.xr));
     return (int)hipGetLastError();
 }
 
@@ -685,7 +720,9 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
         const int Pb = block_size(k, P, bn);
         double* tin = p ? buf1 : buf0;
         double* toth = p ? buf0 : buf1;
-        for (int l = 1; l <= Pb && !err; ++l) {
+        if (!sh && plan_persistent(s))   // the block's Pb planner steps in one launch
+            err = launch_blk_plan(tin, s, Pb, p, bn, ctl, bp, blk, log, xhist, log_cap, st);
+        for (int l = 1; l <= Pb && !err && !(!sh && plan_persistent(s)); ++l) {
             if (sh) {
                 err = launch_bsh_pack(l - 1, tin, s, Pb, bn, ctl, bp, send, st);
                 if (!err && !light) {
@@ -1575,6 +1612,12 @@ int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear) {
 int smx_tune_block_form(int32_t form) {
     const int prev = g_block_form;
     if (form == 0 || form == 4 || form == 5) g_block_form = form;
+    return prev;
+}
+
+int smx_tune_block_persist(int32_t on) {
+    const int prev = g_block_persist;
+    if (on >= 0) g_block_persist = on ? 1 : 0;
     return prev;
 }
 

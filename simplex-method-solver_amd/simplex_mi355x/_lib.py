@@ -68,7 +68,7 @@ EXPORTS = (
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
     "smx_tune_resident", "smx_tune_resident_overlap", "smx_tune_resident_timeout", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check", "smx_fastdiv_check_bounded",
-    "smx_tune_block", "smx_tune_block_pipe", "smx_tune_block_form", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
+    "smx_tune_block", "smx_tune_block_pipe", "smx_tune_block_form", "smx_tune_block_persist", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_graph_create",
@@ -156,6 +156,7 @@ def load():
         "smx_tune_block": ([i32], ctypes.c_int),
         "smx_tune_block_pipe": ([i32], ctypes.c_int),
         "smx_tune_block_form": ([i32], ctypes.c_int),
+        "smx_tune_block_persist": ([i32], ctypes.c_int),
         "smx_block_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
         "smx_block_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp],
                           ctypes.c_int),
@@ -252,6 +253,12 @@ def tune_block(pivots: int = -1) -> int:
     """smx_tune_block: 0 automatic, 1 never, 2..16 pivots per sweep, -1 query only; returns the
     previous setting."""
     return int(load().smx_tune_block(pivots))
+
+
+def tune_block_persist(on: int = -1) -> int:
+    """smx_tune_block_persist: 1 plans each block of an unsharded chain in one persistent launch
+    (k_blk_plan), 0 one launch per pivot (k_blk_step); -1 only queries.  Returns the previous."""
+    return int(load().smx_tune_block_persist(on))
 
 
 def tune_block_form(form: int = -1) -> int:

@@ -411,8 +411,8 @@ class DeviceTableau:
         if int(c["dec"][0][0]) & _lib.RESIDENT_TIMEOUT:
             self._pending = False
             if snap is None:
-                raise RuntimeError("resident pivot loop: a workgroup hand-off timed out (the "
-                                   "tableau on the device is undefined)")
+                raise RuntimeError("a workgroup hand-off timed out (resident pivot loop or "
+                                   "persistent planner; the tableau on the device is undefined)")
             # the chain's workgroups could not all be resident at once (or one stalled): put
             # its input back and run the same pivots on the launch chain, for good on this
             # tableau -- the same decisions and arithmetic, so the same results

@@ -1,5 +1,6 @@
 """GPU parity of block pivots (smx_block_run, csrc/smx_block.hpp): P pivots planned from the
-block's input table and applied in one HBM sweep.  Bit-exact against the golden fixtures, the C
+block's input table and applied in one HBM sweep; every test runs with the planner as one launch
+per pivot and as one persistent launch per block (csrc/smx_plan.hpp).  Bit-exact against the golden fixtures, the C
 oracle and the one-pivot-per-sweep chain, for block sizes 1..24, both sweep layouts (pivot-row
 slices in registers / in LDS, smx_tune_block_form), ragged last blocks, terminal outcomes inside
 a block, the x-history ring and interleaving with host steps.
@@ -19,6 +20,16 @@ def _need_gpu():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs an MI355X")
+
+
+@pytest.fixture(autouse=True, params=[0, 1], ids=["launch", "persist"])
+def planner_form(request):
+    """Every test twice: the planner as one launch per pivot (k_blk_step) and as one persistent
+    launch per block (k_blk_plan, smx_tune_block_persist) -- the same bits either way."""
+    from simplex_mi355x import _lib
+    prev = _lib.tune_block_persist(request.param)
+    yield request.param
+    _lib.tune_block_persist(prev)
 
 
 @pytest.fixture
@@ -266,12 +277,36 @@ def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
     assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
 
 
+@pytest.mark.parametrize("kind,k", [("degenerate", 20), ("degenerate", 41), ("uniform", 20),
+                                    ("degenerate_mixed", 41)])
+def test_block_wide_table_vs_oracle(block_mode, kind, k):
+    """A 1 GiB table 4096 x 32768 (config 5's width: 256 chunks of 128 columns per row) through
+    the default policy, 20 pivots per sweep in the LDS layout, integer degenerate data included
+    (zeros: the zero-extended division; exact paths): 20 = one block, 41 = 14 + 14 + 13."""
+    from simplex_mi355x import lp
+    from simplex_mi355x.device import DeviceTableau
+    from oracle import c_oracle
+    block_mode(0)
+    n, m = 4095, 32767
+    T = lp.dense_tableau(kind, 5, n, m)
+    dev = DeviceTableau(T, n, m, m)
+    assert dev.block_plan()[1] == 20
+    dev.run(k, graph=False)
+    ctl = dev.sync_state()
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=16)
+    assert int(ctl["npivots"]) == done
+    assert np.array_equal(dev.read_log(0, done), log)
+    got = dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
 def test_block_plan_policy(block_mode):
     from simplex_mi355x import _lib
     block_mode(0)
-    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 20   # 1-4 GiB
-    assert _lib.block_plan([32768, 32767, 32767, 32767, 32767, 0, 64])[1] == 12   # 8 GiB
-    assert _lib.block_plan([32768, 65535, 65535, 32767, 32767, 0, 64])[1] == 12   # config 5
+    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 20   # 2 GiB
+    assert _lib.block_plan([32768, 32767, 32767, 32767, 32767, 0, 64])[1] == 20   # 8 GiB
+    assert _lib.block_plan([32768, 65535, 65535, 32767, 32767, 0, 64])[1] == 20   # config 5
     assert _lib.block_plan([8192, 8191, 8191, 8191, 8191, 0, 32])[1] == 12
     assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 10
     assert _lib.block_plan([2048, 2047, 2047, 2047, 2047, 0, 8]) is None    # below 48 MiB
@@ -350,3 +385,30 @@ def test_nofree_knob_with_captured_block_graph():
                          capture_output=True, text=True, timeout=300, cwd=repo)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "nofree ok" in out.stdout
+
+
+def test_persistent_graph_replays_and_tall_fallback(block_mode, planner_form):
+    """The persistent planner's granule tags carry a per-scratch launch count, so replaying ONE
+    captured graph many times never meets a previous replay's records; a table with more rows
+    than planner threads (65,537 > 256 x 256) falls back to one launch per pivot."""
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    import simplex
+    block_mode(6)
+    n, m = 1500, 1100
+    T = lp.dense_tableau("uniform", 21, n, m)
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    sm.solve(record_history=False, max_pivots=120, chunk=12, graph=True)   # 10 replays
+    assert len(sm._dev._graphs) <= 2
+    Tref, st, done, log = c_oracle.run(T, n, m, m, 120, threads=8)
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    got = sm._dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    n, m = 65537, 63
+    T = lp.dense_tableau("uniform", 22, n, m)
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    sm.solve(record_history=False, max_pivots=30, chunk=30)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, 30, threads=8)
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    got = sm._dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))

@@ -27,6 +27,9 @@ def main() -> None:
     ap.add_argument("--bpc", type=int, default=0, help="blocks per CU of the sweep (0: library)")
     ap.add_argument("--pipe", default="0", help="smx_tune_block_pipe settings to compare, e.g. 1,0")
     ap.add_argument("--form", default="0", help="smx_tune_block_form settings to compare, e.g. 4,5")
+    ap.add_argument("--persist", default="0",
+                    help="smx_tune_block_persist settings to compare (planner: 0 one launch per "
+                         "pivot, 1 one persistent launch per block), e.g. 0,1")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -41,11 +44,13 @@ def main() -> None:
         dev = DeviceTableau(T, n, m, m, block=0)
         k = a.k
         ref_log = ref_tab = None
-        runs = [(0, 0, 0)] + [(int(x), int(pp), int(f)) for x in a.pivots.split(",")
-                              for pp in a.pipe.split(",") for f in a.form.split(",")]
-        for P, pipe, form in runs:
+        runs = [(0, 0, 0, 0)] + [(int(x), int(pp), int(f), int(ps))
+                                 for x in a.pivots.split(",") for pp in a.pipe.split(",")
+                                 for f in a.form.split(",") for ps in a.persist.split(",")]
+        for P, pipe, form, persist in runs:
             _lib.tune_block_pipe(pipe)
             _lib.tune_block_form(form)
+            _lib.tune_block_persist(persist)
             dev.close()   # captured graphs bake in the layout: capture afresh for every run
             dev.block = P
             dev.upload(T)
@@ -66,7 +71,7 @@ def main() -> None:
             log = dev.read_log(0, int(ctl["npivots"]))
             tab = dev.download().view(np.int64)
             row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "pipe": pipe,
-                   "form": form, "k": k,
+                   "form": form, "persist": persist, "k": k,
                    "bpc": a.bpc,
                    "us_per_pivot": ms * 1e3 / k, "pivots_s": k / ms * 1e3,
                    "npivots": int(ctl["npivots"])}
