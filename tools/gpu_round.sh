@@ -16,6 +16,7 @@
 #                          GRBM_COUNT SQ_INSTS_VALU SQ_BUSY_CYCLES of bench200 (the clock per sweep)
 #   paths=ARGS             tools/sweep_paths.py ARGS on the diagnostic build (libsmx_diag.so)
 #   sweeps=ARGS            tools/sweep_paths.py ARGS on the product build (timings only)
+#   sweepslib=LIB,ARGS     tools/sweep_paths.py ARGS on another build of libsmx (SMX_LIB=LIB: an A/B)
 #   blockbench=ARGS        tools/block_bench.py ARGS
 #   configs=ARGS           tools/run_configs.py ARGS
 #   py=SCRIPT,ARGS         python3 SCRIPT ARGS (a tools/ probe)
@@ -59,6 +60,7 @@ for spec in "$@"; do
     clock200) cmd="cd /tmp && timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VALU SQ_BUSY_CYCLES -d $O/clock200 -o run --output-format csv -- $B --steps 200 --warmup 20"; d=300 ;;
     paths) cmd="cd $R && SMX_LIB=libsmx_diag.so python -u tools/sweep_paths.py $arg"; d=300 ;;
     sweeps) cmd="cd $R && python -u tools/sweep_paths.py $arg"; d=300 ;;
+    sweepslib) lib="${arg%% *}"; cmd="cd $R && SMX_LIB=$lib python -u tools/sweep_paths.py ${arg#* }"; d=300 ;;
     blockbench) cmd="cd $R && python -u tools/block_bench.py $arg"; d=400 ;;
     configs) cmd="cd $R && python -u tools/run_configs.py $arg"; d=600 ;;
     py) cmd="cd $R && python -u $arg"; d=300 ;;
