@@ -224,17 +224,10 @@ __device__ __forceinline__ bool bnd_or_zero(double v) {
 __device__ __forceinline__ double fd_zero(double n, double e, double y) {
     const double t = n * y;
     const double r = fma(-e, t, n);
-    const double q = fma(r, y, t);
-#ifdef SMX_FDZERO_FIXUP
-    return __builtin_amdgcn_div_fixup(q, e, n);
-#else
-    // The same result without v_div_fixup_f64 (several issue slots on gfx950: the zero-extended
-    // path ran ~1.7x the fast path's time per unit, profiles/r05a/): a zero numerator gives a
-    // zero q (r = +0 then) whose only wrong bit can be the sign, and t = n y is that zero with
-    // the right sign, sign(n) xor sign(e) -- so the high dword comes from t there.
-    const int hi = (n == 0.0) ? __double2hiint(t) : __double2hiint(q);
-    return __hiloint2double(hi, __double2loint(q));
-#endif
+    // (Round 5 tried the sign fix as a compare + a 32-bit select of t's high dword instead: the
+    // zero-extended path ran no faster and the whole sweep kernel 5 % slower on the steady-state
+    // config-5 blocks, profiles/r05d/.)
+    return __builtin_amdgcn_div_fixup(fma(r, y, t), e, n);
 }
 
 // Self-check of the unchecked sequences on the domains the bounds guarantee (smx_fastdiv_check
@@ -781,6 +774,7 @@ __device__ __forceinline__ bool blk_step_body(
     constexpr int SCANU = LAG ? 1 : 4;
     constexpr int NQ = 2 * kBlkMax + 1;
     __shared__ BlkPiv s_pv;
+    __shared__ int s_okd;
     __shared__ double s_col[3][kBlkMax];      // pr_q at columns c, m, cf
     // LAG: the chain's pivots (previous block's, then this block's), row r's multipliers, the
     // pr_q values at columns c, m, cf, and one operand row per thread
@@ -904,9 +898,26 @@ __device__ __forceinline__ bool blk_step_body(
 #pragma unroll
         for (int q = 0; q < D; ++q) blk_pin(mqr[q]);
     }
-    // this block's first D pivots in registers (s_pv is complete up to D since the decision)
+    // this block's first D pivots (s_pv is complete up to D since the decision)
     bool okD = true;
+#ifdef SMX_PLAN_LDS
+    // read from LDS where the chains use them (uniform operands: broadcast reads), instead of
+    // pinned register copies -- six VGPRs per pivot that pushed the step kernels past 256
+    // architectural VGPRs into AGPR shuffles and early waits from ~10 pivots on
+    if constexpr (!LAG) {
+        if (tid < kWave) {
+            const bool bad = tid < D && (!fd_prep(s_pv.e[tid]).ok);
+            const uint64_t mk = __ballot(bad);
+            if (tid < D) s_pv.y[tid] = fd_prep(s_pv.e[tid]).y;
+            if (tid == 0) s_okd = mk == 0;
+        }
+        __syncthreads();
+        okD = s_okd != 0;
+    }
+    const BlkPiv& pvD = s_pv;
+#else
     const BlkPiv pvD = blk_pv_regs<D>(s_pv, &okD);
+#endif
     auto prv = [&](int j) -> double {
         if (SH) return prow[j];
         if constexpr (LAG) {
@@ -1165,6 +1176,11 @@ __device__ __forceinline__ bool blk_step_body(
             s_pv.r[D] = r_local;
             s_pv.c[D] = c;
             s_pv.e[D] = e;
+#ifdef SMX_PLAN_LDS
+            const FastDiv fdl = fd_prep(e);
+            s_pv.y[D] = fdl.y;
+            s_okd = (s_okd != 0 && fdl.ok) ? 1 : 0;
+#endif
             s_col[1][D] = s_pm;
             s_col[2][D] = s_pa;
         }
@@ -1187,6 +1203,11 @@ __device__ __forceinline__ bool blk_step_body(
     // column in phase 2 -- is kept from the step that read it: one strided column per step
     // instead of three.
     // the row pass's shared operands in registers: the L pivots and the pivot rows at c, m, cf
+#ifdef SMX_PLAN_LDS
+    const BlkPiv& pvL = s_pv;
+    const bool okL = LAG ? true : s_okd != 0;
+    auto& colv = s_col;
+#else
     BlkPiv pvL;
     bool okL = true;
     double colv[3][kBlkMax];
@@ -1200,6 +1221,7 @@ __device__ __forceinline__ bool blk_step_body(
             for (int q = 0; q < L; ++q) blk_pin(colv[k][q]);
         }
     }
+#endif
     // Chain-result cache (the register form): step L keeps T_{k+L}[i][m] and T_{k+L}[i][cf] --
     // the values its records were built on -- in cb / ca by step parity, so step L+1 takes its
     // multipliers T_{k+L}[i][c] (c = this cf in phase 2) as they are and its "-b" values with ONE
@@ -1592,15 +1614,32 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
             // arithmetic with fd_zero's v_div_fixup (ONE more instruction per element-pivot)
             asm volatile("" ::: "memory");   // keeps this path out of the fast path's code
             SMX_PC(kPcZero);
+            if constexpr (!LDS) {
+                // the 2P products first, as on the fast path (they do not depend on the chain)
+                dbl2 bq[P];
 #pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const dbl2 p = PR(q);
-                const dbl2 ey = EY(q);
-                const double e = ey[0], y = ey[1];
-                double n[2];
-                n[0] = v0[0] * e - p[0] * pc0[q];
-                n[1] = v0[1] * e - p[1] * pc0[q];
-                v0 = dbl2{fd_zero(n[0], e, y), fd_zero(n[1], e, y)};
+                for (int q = 0; q < P; ++q)
+                    bq[q] = dbl2{prs[q][0] * pc0[q], prs[q][1] * pc0[q]};
+#pragma unroll
+                for (int q = 0; q < P; ++q) asm volatile("" : "+v"(bq[q]));
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    const double e = eq[q], y = yq[q];
+                    const double n0 = v0[0] * e - bq[q][0];
+                    const double n1 = v0[1] * e - bq[q][1];
+                    v0 = dbl2{fd_zero(n0, e, y), fd_zero(n1, e, y)};
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    const dbl2 p = PR(q);
+                    const dbl2 ey = EY(q);
+                    const double e = ey[0], y = ey[1];
+                    double n[2];
+                    n[0] = v0[0] * e - p[0] * pc0[q];
+                    n[1] = v0[1] * e - p[1] * pc0[q];
+                    v0 = dbl2{fd_zero(n[0], e, y), fd_zero(n[1], e, y)};
+                }
             }
             ok = true;
         } else if (allok && rf != 2) {   // not a pivot row (rf == 2): the window-tracked path

@@ -348,11 +348,16 @@ bool resident_plan(const smx_shape& s, ResPlan* p) {
     if (s.m + 1 > 4096) return false;   // 13-bit phase-1 column in the record
     const int C = s.m + 1;
     // automatic: about four rows per workgroup (tools/resident_bench.py: 256^2 64 groups, 512^2
-    // 128, 1024^2 256), more when the rows do not fit in LDS, at most one workgroup per CU
+    // 128, 1024^2 256), six where the overlapped loop runs (its update hides under the poll, so
+    // fewer records to poll pay: 1024^2 8.72 / 8.73 / 8.26 / 8.55 us per pivot at 4 / 8 / 6 / 5
+    // rows per workgroup, profiles/r05d/), more when the rows do not fit in LDS, at most one
+    // workgroup per CU
     const int64_t ldl = C | 1;
     auto lds_of = [&](int r) { return ((int64_t)(r + 1) * ldl + C + (r + 1)) * 8; };
     const int gmax = g_resident > 0 ? g_resident : (num_cus() < kResPollers ? num_cus() : kResPollers);
-    int G = g_resident > 0 ? g_resident : (s.n + 3) / 4;
+    const bool ovl = g_resident_ovl == 1 || (g_resident_ovl == 2 && C >= kResOvlMinCols);
+    const int per = ovl ? 6 : 4;
+    int G = g_resident > 0 ? g_resident : (s.n + per - 1) / per;
     if (G > gmax) G = gmax;
     if (G > s.n) G = s.n;
     int rpw = (s.n + G - 1) / G;

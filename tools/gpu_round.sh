@@ -18,6 +18,7 @@
 #   sweeps=ARGS            tools/sweep_paths.py ARGS on the product build (timings only)
 #   sweepslib=LIB,ARGS     tools/sweep_paths.py ARGS on another build of libsmx (SMX_LIB=LIB: an A/B)
 #   blockbench=ARGS        tools/block_bench.py ARGS
+#   blockbenchlib=LIB,ARGS tools/block_bench.py ARGS on another build of libsmx (SMX_LIB=LIB)
 #   configs=ARGS           tools/run_configs.py ARGS
 #   py=SCRIPT,ARGS         python3 SCRIPT ARGS (a tools/ probe)
 # A recipe may carry its own time limit: `paths=...@300` (seconds; default per recipe below).
@@ -62,6 +63,7 @@ for spec in "$@"; do
     sweeps) cmd="cd $R && python -u tools/sweep_paths.py $arg"; d=300 ;;
     sweepslib) lib="${arg%% *}"; cmd="cd $R && SMX_LIB=$lib python -u tools/sweep_paths.py ${arg#* }"; d=300 ;;
     blockbench) cmd="cd $R && python -u tools/block_bench.py $arg"; d=400 ;;
+    blockbenchlib) lib="${arg%% *}"; cmd="cd $R && SMX_LIB=$lib python -u tools/block_bench.py ${arg#* }"; d=400 ;;
     configs) cmd="cd $R && python -u tools/run_configs.py $arg"; d=600 ;;
     py) cmd="cd $R && python -u $arg"; d=300 ;;
     *) echo "unknown recipe $name"; exit 2 ;;
