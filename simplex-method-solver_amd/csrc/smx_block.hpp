@@ -774,7 +774,6 @@ __device__ __forceinline__ bool blk_step_body(
     constexpr int SCANU = LAG ? 1 : 4;
     constexpr int NQ = 2 * kBlkMax + 1;
     __shared__ BlkPiv s_pv;
-    __shared__ int s_okd;
     __shared__ double s_col[3][kBlkMax];      // pr_q at columns c, m, cf
     // LAG: the chain's pivots (previous block's, then this block's), row r's multipliers, the
     // pr_q values at columns c, m, cf, and one operand row per thread
@@ -900,24 +899,7 @@ __device__ __forceinline__ bool blk_step_body(
     }
     // this block's first D pivots (s_pv is complete up to D since the decision)
     bool okD = true;
-#ifdef SMX_PLAN_LDS
-    // read from LDS where the chains use them (uniform operands: broadcast reads), instead of
-    // pinned register copies -- six VGPRs per pivot that pushed the step kernels past 256
-    // architectural VGPRs into AGPR shuffles and early waits from ~10 pivots on
-    if constexpr (!LAG) {
-        if (tid < kWave) {
-            const bool bad = tid < D && (!fd_prep(s_pv.e[tid]).ok);
-            const uint64_t mk = __ballot(bad);
-            if (tid < D) s_pv.y[tid] = fd_prep(s_pv.e[tid]).y;
-            if (tid == 0) s_okd = mk == 0;
-        }
-        __syncthreads();
-        okD = s_okd != 0;
-    }
-    const BlkPiv& pvD = s_pv;
-#else
     const BlkPiv pvD = blk_pv_regs<D>(s_pv, &okD);
-#endif
     auto prv = [&](int j) -> double {
         if (SH) return prow[j];
         if constexpr (LAG) {
@@ -1176,11 +1158,6 @@ __device__ __forceinline__ bool blk_step_body(
             s_pv.r[D] = r_local;
             s_pv.c[D] = c;
             s_pv.e[D] = e;
-#ifdef SMX_PLAN_LDS
-            const FastDiv fdl = fd_prep(e);
-            s_pv.y[D] = fdl.y;
-            s_okd = (s_okd != 0 && fdl.ok) ? 1 : 0;
-#endif
             s_col[1][D] = s_pm;
             s_col[2][D] = s_pa;
         }
@@ -1203,11 +1180,6 @@ __device__ __forceinline__ bool blk_step_body(
     // column in phase 2 -- is kept from the step that read it: one strided column per step
     // instead of three.
     // the row pass's shared operands in registers: the L pivots and the pivot rows at c, m, cf
-#ifdef SMX_PLAN_LDS
-    const BlkPiv& pvL = s_pv;
-    const bool okL = LAG ? true : s_okd != 0;
-    auto& colv = s_col;
-#else
     BlkPiv pvL;
     bool okL = true;
     double colv[3][kBlkMax];
@@ -1221,7 +1193,6 @@ __device__ __forceinline__ bool blk_step_body(
             for (int q = 0; q < L; ++q) blk_pin(colv[k][q]);
         }
     }
-#endif
     // Chain-result cache (the register form): step L keeps T_{k+L}[i][m] and T_{k+L}[i][cf] --
     // the values its records were built on -- in cb / ca by step parity, so step L+1 takes its
     // multipliers T_{k+L}[i][c] (c = this cf in phase 2) as they are and its "-b" values with ONE

@@ -289,7 +289,7 @@ def test_two_resident_chains_on_separate_streams(resident_mode):
     from simplex_mi355x import lp
     from simplex_mi355x.device import DeviceTableau
     import torch
-    resident_mode(0)
+    resident_mode(256)   # every CU: two such chains can never be resident together
     n = m = 1023
     k = 150
     Ts = [lp.dense_tableau(kind, 21, n, m) for kind in ("uniform", "mixed")]
