@@ -134,7 +134,7 @@ def test_config5_sharded_65536x32768(kind):
     n, m, world, P = 65535, 32767, 8, 8
     T = lp.dense_tableau(kind, 0, n, m)
     dev = DeviceTableau(T, n, m, m, log_cap=1 << 12)
-    assert dev.block_plan()[1] == 12           # the unsharded path: up to 12 pivots per sweep
+    assert dev.block_plan()[1] == 20           # the unsharded path: up to 20 pivots per sweep (8 GiB)
     bes = _backends(T, n, m, world, P)
 
     # 9-pivot prefix (sharded: a block of 8 + a ragged 1; unsharded: one block) against the C

@@ -21,6 +21,7 @@
 #   blockbenchlib=LIB,ARGS tools/block_bench.py ARGS on another build of libsmx (SMX_LIB=LIB)
 #   configs=ARGS           tools/run_configs.py ARGS
 #   py=SCRIPT,ARGS         python3 SCRIPT ARGS (a tools/ probe)
+#   run=PROGRAM,ARGS       a built tools/ probe (e.g. `run=tools/cumask_probe`)
 # A recipe may carry its own time limit: `paths=...@300` (seconds; default per recipe below).
 set -o pipefail
 TAG=${1:?tag}
@@ -66,6 +67,7 @@ for spec in "$@"; do
     blockbenchlib) lib="${arg%% *}"; cmd="cd $R && SMX_LIB=$lib python -u tools/block_bench.py ${arg#* }"; d=400 ;;
     configs) cmd="cd $R && python -u tools/run_configs.py $arg"; d=600 ;;
     py) cmd="cd $R && python -u $arg"; d=300 ;;
+    run) cmd="cd $R && $arg"; d=300 ;;
     *) echo "unknown recipe $name"; exit 2 ;;
   esac
   STEPS+=("$tag|${lim:-$d}|$cmd")
