@@ -369,6 +369,14 @@ int smx_tune_block_persist(int32_t on);
  * chain.  0 plans each block on the caller's stream before its sweep.  -1 keeps the setting;
  * returns the previous one. */
 int smx_tune_block_pipe(int32_t on);
+/* CU partition of pipelined chains (default 0, 0): cus_per_xcd > 0 runs the planner on that many
+ * CUs of every XCD and the sweeps on the rest (two CU-masked library streams; the caller's stream
+ * forks to the sweep stream and joins it at the end of the chain), so the planner neither waits
+ * for a sweep's waves nor shares their CUs; parts > 0 caps the planner's workgroups so they fit
+ * on its CUs.  MI355X only (256 CUs); a chain enqueued under stream capture runs unpartitioned
+ * (graph kernel nodes do not keep a stream's CU mask).  -1 keeps a setting; returns the previous
+ * cus_per_xcd, or -1 for an out-of-range value (nothing changed). */
+int smx_tune_block_pipe_cus(int32_t cus_per_xcd, int32_t parts);
 int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout);
 int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
                   int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log,

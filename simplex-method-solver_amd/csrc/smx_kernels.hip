@@ -185,6 +185,7 @@ int variant_for(const smx_shape& s) {
 // is resident at once and the balanced unit ranges finish together (no second residency round).
 // The host-side caches below are shared by smx_mshard_run's per-device threads: one mutex.
 std::mutex g_cache_mu;
+std::mutex g_pipe_mu;   // the pipelined chains' per-device streams (blk_pipe_for)
 
 // Resident 256-thread blocks per CU of `fn` by the occupancy API (registers and LDS), one block
 // of margin below its answer, cached; at most `cap`.
@@ -219,7 +220,11 @@ int resident_bpc(const void* fn, int cap) {
     return bpc < cap ? bpc : cap;
 }
 
+// CUs the launches of this thread may fill: the device's, or fewer while a pipelined chain runs
+// its sweeps on a CU-masked stream (CusScope)
+thread_local int t_cus = 0;
 int num_cus() {
+    if (t_cus > 0) return t_cus;
     static int cus[64] = {0};
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -562,6 +567,15 @@ struct BlkPtrs {
     smx_part* parts;
     double *mul[2], *pr[2], *fr;
 };
+// Planner workgroups of a launch: blk_parts_of, or fewer in a pipelined chain whose planner runs
+// on a few CUs of its own (t_parts_cap; every launch of one chain uses the same count, since a
+// step merges the records of the step before it by that count)
+thread_local int t_parts_cap = 0;
+int blk_G(const smx_shape& s) {
+    const int g = blk_parts_of(s.nparts, s.rows);
+    return t_parts_cap > 0 && t_parts_cap < g ? t_parts_cap : g;
+}
+
 BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
     BlkPtrs b;
     b.L = blk_layout(s.rows + 1, s.ld, blk_parts_of(s.nparts, s.rows));
@@ -580,7 +594,7 @@ int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, s
                      const BlkPtrs& b, hipStream_t st) {
     hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, T, s.ld, s.rows, s.m,
                        fscan_of(s), parity, loc, (const smx_ctl*)ctl, b.h[0], b.h[1], b.fr);
-    hipLaunchKernelGGL(k_blk_first, dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
+    hipLaunchKernelGGL(k_blk_first, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
                        s.row0, (const smx_ctl*)ctl, (const BlkHdr*)b.h[0], b.parts);
     return (int)hipGetLastError();
 }
@@ -594,7 +608,7 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
     BlkStepFn fn = sh ? blk_step_fn_sh<true, false>(L)
                       : (pp > 0 ? blk_step_fn_sh<false, true>(L) : blk_step_fn_sh<false, false>(L));
     const int o = slot ^ 1;
-    hipLaunchKernelGGL(fn, dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
+    hipLaunchKernelGGL(fn, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
                        fscan_of(s), s.row0, P, parity, bn, ctl, b.h[slot], b.h[0], b.parts,
                        b.mul[slot], b.pr[slot], b.fr, recv, nranks, log, xhist, log_cap,
                        (const BlkHdr*)b.h[o], (const double*)b.mul[o], (const double*)b.pr[o],
@@ -642,7 +656,7 @@ int launch_blk_plan(const double* T, const smx_shape& s, int P, int parity, int 
 int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, const BlkPtrs& b,
                        hipStream_t st) {
     hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)b.h[0],
-                       (const smx_part*)b.parts, blk_parts_of(s.nparts, s.rows), blk_slot(0, 1, bn), parity, ctl);
+                       (const smx_part*)b.parts, blk_G(s), blk_slot(0, 1, bn), parity, ctl);
     return (int)hipGetLastError();
 }
 
@@ -700,6 +714,113 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     return (int)hipGetLastError();
 }
 
+// smx_tune_block_pipe: 1 plans block b+1 on a second stream while block b is swept;
+// 0 (default) plans every block on the solver stream right before its sweep.
+int g_block_pipe = 0;
+
+// smx_tune_block_pipe_cus: r > 0 gives the planner of a pipelined chain r CUs of every XCD and
+// the sweeps the other 32 - r (two CU-masked streams, hipExtStreamCreateWithCUMask), so the
+// planner's launches neither wait for the sweep's waves to retire nor share their CUs' issue
+// slots; parts > 0 caps the planner's workgroups (every launch of such a chain) so they all fit
+// on the planner's CUs at once.  MI355X only (256 CUs, 8 XCDs of 32); eager chains only -- a
+// captured graph's kernel nodes do not keep their stream's CU mask, so a chain enqueued under
+// stream capture runs unpartitioned.
+int g_pipe_cus = 0, g_pipe_parts = 0;
+
+// CU mask of the planner (r per XCD) or of the sweeps (the rest): bits {32x + x + 8t : x < 8,
+// t < r} -- r CUs of every XCD whether the driver maps mask bit i to XCD i / 32 or to XCD i % 8
+// (tools/cumask_probe.hip)
+void pipe_cu_mask(int r, bool planner, uint32_t m[8]) {
+    for (int w = 0; w < 8; ++w) m[w] = planner ? 0u : ~0u;
+    for (int x = 0; x < 8; ++x)
+        for (int t = 0; t < r; ++t) {
+            const int i = 32 * x + x + 8 * t;
+            if (planner) m[i / 32] |= 1u << (i % 32);
+            else m[i / 32] &= ~(1u << (i % 32));
+        }
+}
+
+// The planner stream (and, partitioned, the sweep stream) and the events ordering them against
+// the solver stream, once per device and partition.
+struct BlkPipe {
+    hipStream_t q = nullptr, sw = nullptr;
+    int r = -1;   // the partition q / sw were made for (0: unmasked planner stream, no sw)
+    hipEvent_t fork = nullptr, join = nullptr, plan[2] = {nullptr, nullptr},
+               sweep[2] = {nullptr, nullptr};
+};
+
+// *part: the chain may use the partition (q and sw CU-masked; never under stream capture, which
+// keeps the streams it finds -- nothing may be synchronised or destroyed while capturing)
+int blk_pipe_for(hipStream_t st, BlkPipe** out, bool* part) {
+    static BlkPipe cache[64];
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cap);
+    const bool capturing = cap != hipStreamCaptureStatusNone;
+    const int ncu = num_cus();
+    std::lock_guard<std::mutex> lock(g_pipe_mu);
+    BlkPipe& o = cache[dev];
+    const int r = capturing && o.q ? o.r : (!capturing && ncu == 256 ? g_pipe_cus : 0);
+    *part = !capturing && r > 0;
+    if (o.q && o.r == r) {
+        *out = &o;
+        return 0;
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    hipError_t e = hipSetDevice(dev);
+    if (o.q) {   // another partition: new streams (the old ones are drained first)
+        if (e == hipSuccess) e = hipStreamSynchronize(o.q);
+        if (e == hipSuccess && o.sw) e = hipStreamSynchronize(o.sw);
+        if (e == hipSuccess) {
+            (void)hipStreamDestroy(o.q);
+            if (o.sw) (void)hipStreamDestroy(o.sw);
+            o.q = o.sw = nullptr;
+        }
+    }
+    if (e == hipSuccess && r > 0) {
+        uint32_t mq[8], ms[8];
+        pipe_cu_mask(r, true, mq);
+        pipe_cu_mask(r, false, ms);
+        e = hipExtStreamCreateWithCUMask(&o.q, 8, mq);
+        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&o.sw, 8, ms);
+    } else if (e == hipSuccess) {
+        e = hipStreamCreateWithFlags(&o.q, hipStreamNonBlocking);
+    }
+    if (e == hipSuccess && !o.fork) {
+        hipEvent_t* evs[6] = {&o.fork, &o.join, &o.plan[0], &o.plan[1], &o.sweep[0], &o.sweep[1]};
+        for (int i = 0; i < 6 && e == hipSuccess; ++i)
+            e = hipEventCreateWithFlags(evs[i], hipEventDisableTiming);
+    }
+    (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+        if (o.q) (void)hipStreamDestroy(o.q);
+        if (o.sw) (void)hipStreamDestroy(o.sw);
+        o.q = o.sw = nullptr;
+        o.r = -1;
+        *part = false;
+        return (int)e;
+    }
+    o.r = r;
+    *out = &o;
+    return 0;
+}
+
+// the CU count (num_cus) and planner workgroup cap (blk_G) of this thread's launches, for a scope
+struct LaunchScope {
+    int cus0, parts0;
+    LaunchScope(int cus, int parts) : cus0(t_cus), parts0(t_parts_cap) {
+        t_cus = cus;
+        t_parts_cap = parts;
+    }
+    ~LaunchScope() {
+        t_cus = cus0;
+        t_parts_cap = parts0;
+    }
+};
+
 // k pivots in blocks of P: prime + first records, then per block P step launches and one sweep;
 // publish.  ev (optional): 2 events per block recorded around its sweep.  With comm (row-sharded,
 // one rank per GPU): every step launch is preceded by this rank's pack and ONE ncclAllGather of
@@ -716,6 +837,14 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     int rank = 0;
     if (light && ncclCommUserRank(comm, &rank) != ncclSuccess) return (int)hipErrorInvalidValue;
     double* xrow = light ? recv + (size_t)nranks * SMX_SHARD_HDR : nullptr;
+    BlkPipe* sqp = nullptr;
+    bool part = false;
+    if (!sh && !g_block_pipe && g_pipe_cus > 0 && !plan_persistent(s)) {
+        const int e = blk_pipe_for(st, &sqp, &part);
+        if (e) return e;
+        if (!part) sqp = nullptr;
+    }
+    LaunchScope scope(0, sqp ? g_pipe_parts : 0);
     int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, parity, ctl, bp, st);
     int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
@@ -727,6 +856,14 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
         double* toth = p ? buf0 : buf1;
         if (!sh && plan_persistent(s))   // the block's Pb planner steps in one launch
             err = launch_blk_plan(tin, s, Pb, p, bn, ctl, bp, blk, log, xhist, log_cap, st);
+        // diagnostic (smx_tune_block_pipe_cus without pipelining): the planner steps on the
+        // partition's planner CUs, in turn with the sweeps (its time on those CUs alone)
+        hipStream_t pst = st;
+        if (sqp && !err) {
+            err = (int)hipEventRecord(sqp->fork, st);
+            if (!err) err = (int)hipStreamWaitEvent(sqp->q, sqp->fork, 0);
+            pst = sqp->q;
+        }
         for (int l = 1; l <= Pb && !err && !(!sh && plan_persistent(s)); ++l) {
             if (sh) {
                 err = launch_bsh_pack(l - 1, tin, s, Pb, bn, ctl, bp, send, st);
@@ -746,7 +883,7 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
             }
             if (!err)   // sharded: each rank writes the x-history of the label rows it owns
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
-                                      xhist, log_cap, st, 0, 0, xrow,
+                                      xhist, log_cap, pst, 0, 0, xrow,
                                       light ? (int64_t)SMX_SHARD_HDR : 0);
 #ifdef SMX_BLK_TRACE_TWICE
             // diagnostic build (tools/trace_planner.hip): a step is idempotent (it reads slot D /
@@ -755,6 +892,10 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
                                       xhist, log_cap, st, 0, 0, xrow, 0);
 #endif
+        }
+        if (sqp && !err) {
+            err = (int)hipEventRecord(sqp->plan[0], sqp->q);
+            if (!err) err = (int)hipStreamWaitEvent(st, sqp->plan[0], 0);
         }
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
         if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st, 0, 0, p);
@@ -768,39 +909,6 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
 }
 
 // ---- pipelined block chains (unsharded) ------------------------------------------------------
-// smx_tune_block_pipe: 1 plans block b+1 on a second stream while block b is swept;
-// 0 (default) plans every block on the solver stream right before its sweep.
-int g_block_pipe = 0;
-
-// The planner stream and the events ordering it against the solver stream, once per device.
-struct BlkPipe {
-    hipStream_t q = nullptr;
-    hipEvent_t fork = nullptr, plan[2] = {nullptr, nullptr}, sweep[2] = {nullptr, nullptr};
-};
-
-int blk_pipe_for(hipStream_t st, BlkPipe** out) {
-    static BlkPipe cache[64];
-    int dev = 0;
-    if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
-    BlkPipe& o = cache[dev];
-    if (!o.q) {
-        int cur = 0;
-        (void)hipGetDevice(&cur);
-        hipError_t e = hipSetDevice(dev);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&o.q, hipStreamNonBlocking);
-        hipEvent_t* evs[5] = {&o.fork, &o.plan[0], &o.plan[1], &o.sweep[0], &o.sweep[1]};
-        for (int i = 0; i < 5 && e == hipSuccess; ++i)
-            e = hipEventCreateWithFlags(evs[i], hipEventDisableTiming);
-        (void)hipSetDevice(cur);
-        if (e != hipSuccess) {
-            o.q = nullptr;
-            return (int)e;
-        }
-    }
-    *out = &o;
-    return 0;
-}
 
 // k pivots in blocks of P with the planner off the critical path:
 //   solver stream S: prime; plan block 0 (its steps, from X_0); then per block b:
@@ -815,8 +923,14 @@ int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int 
                             int P, smx_ctl* ctl, char* blk, int32_t* log, double* xhist,
                             int64_t log_cap, hipStream_t st, hipEvent_t* ev = nullptr) {
     BlkPipe* pp = nullptr;
-    int err = blk_pipe_for(st, &pp);
+    bool part = false;
+    int err = blk_pipe_for(st, &pp, &part);
     if (err) return err;
+    // partitioned: the solver stream forks to the sweep stream (sized grids: num_cus() below is
+    // the sweep's CU count) and joins it at the end
+    const int ncu = num_cus();
+    LaunchScope scope(part ? ncu - 8 * pp->r : 0, g_pipe_parts);
+    hipStream_t S = part ? pp->sw : st;
     const BlkPtrs bp = blk_ptrs(s, blk);
     const int nb = (k + P - 1) / P;
     const int P0 = k - (nb - 1) * P;
@@ -824,12 +938,16 @@ int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int 
     auto hip = [&](hipError_t e) {
         if (!err && e != hipSuccess) err = (int)e;
     };
-    err = launch_blk_prime(buf(parity), s, parity, parity, ctl, bp, st);
+    if (part) {
+        hip(hipEventRecord(pp->fork, st));
+        hip(hipStreamWaitEvent(S, pp->fork, 0));
+    }
+    if (!err) err = launch_blk_prime(buf(parity), s, parity, parity, ctl, bp, S);
     for (int l = 1; l <= P0 && !err; ++l)
         err = launch_blk_step(false, l, buf(parity), s, P0, parity, 0, ctl, bp, nullptr, 0, log,
-                              xhist, log_cap, st);
+                              xhist, log_cap, S);
     if (nb > 1) {
-        hip(hipEventRecord(pp->fork, st));
+        hip(hipEventRecord(pp->fork, S));
         hip(hipStreamWaitEvent(pp->q, pp->fork, 0));
     }
     int db = 0;   // pivots before block b
@@ -838,14 +956,14 @@ int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int 
         const int in_idx = (parity + b) & 1;
         const bool last = b == nb - 1;
         const int x = (db - b) & 1;   // blk_out: in place iff x + (pivots applied) is even
-        if (b > 0) hip(hipStreamWaitEvent(st, pp->plan[b & 1], 0));
-        if (ev) hip(hipEventRecord(ev[2 * b], st));
+        if (b > 0) hip(hipStreamWaitEvent(S, pp->plan[b & 1], 0));
+        if (ev) hip(hipEventRecord(ev[2 * b], S));
         if (!err)
-            err = launch_block_sweep(buf(in_idx), buf(in_idx ^ 1), s, Pb, blk, bp.L, st, b & 1,
+            err = launch_block_sweep(buf(in_idx), buf(in_idx ^ 1), s, Pb, blk, bp.L, S, b & 1,
                                      last ? x : -1, in_idx, x);
-        if (ev) hip(hipEventRecord(ev[2 * b + 1], st));
+        if (ev) hip(hipEventRecord(ev[2 * b + 1], S));
         if (!last) {
-            hip(hipEventRecord(pp->sweep[b & 1], st));
+            hip(hipEventRecord(pp->sweep[b & 1], S));
             if (b >= 1) hip(hipStreamWaitEvent(pp->q, pp->sweep[(b - 1) & 1], 0));
             const int pnext = (parity + db + Pb) & 1;   // pivot parity at block b+1's start
             for (int l = 1; l <= P && !err; ++l)
@@ -855,13 +973,18 @@ int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int 
         }
         db += Pb;
     }
-    if (err) return err;
-    err = launch_blk_publish(s, (parity + k) & 1, nb, ctl, bp, st);
-    if (err) return err;
-    hipLaunchKernelGGL(k_blk_settle, dim3(num_cus() * 4), dim3(kUpdBlock), 0, st, buf0, buf1,
-                       (int64_t)(s.rows + 1) * s.ld, parity, (const smx_ctl*)ctl,
-                       (const BlkHdr*)bp.h[0]);
-    return (int)hipGetLastError();
+    if (!err) err = launch_blk_publish(s, (parity + k) & 1, nb, ctl, bp, S);
+    if (!err)
+        hipLaunchKernelGGL(k_blk_settle, dim3(num_cus() * 4), dim3(kUpdBlock), 0, S, buf0, buf1,
+                           (int64_t)(s.rows + 1) * s.ld, parity, (const smx_ctl*)ctl,
+                           (const BlkHdr*)bp.h[0]);
+    if (!err) err = (int)hipGetLastError();
+    if (part) {   // join (also after an error: the solver stream must not run ahead of S)
+        const hipError_t e1 = hipEventRecord(pp->join, S);
+        const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, pp->join, 0) : e1;
+        if (!err && e2 != hipSuccess) err = (int)e2;
+    }
+    return err;
 }
 
 // The block chain of smx_block_run: pipelined when enabled and there is more than one block.
@@ -1629,6 +1752,14 @@ int smx_tune_block_persist(int32_t on) {
 int smx_tune_block_pipe(int32_t on) {
     const int prev = g_block_pipe;
     if (on >= 0) g_block_pipe = on ? 1 : 0;
+    return prev;
+}
+
+int smx_tune_block_pipe_cus(int32_t cus_per_xcd, int32_t parts) {
+    if (cus_per_xcd > 16 || parts > kBlkPartsMax) return -1;
+    const int prev = g_pipe_cus;
+    if (cus_per_xcd >= 0) g_pipe_cus = cus_per_xcd;
+    if (parts >= 0) g_pipe_parts = parts;
     return prev;
 }
 

@@ -68,7 +68,7 @@ EXPORTS = (
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
     "smx_tune_resident", "smx_tune_resident_overlap", "smx_tune_resident_timeout", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check", "smx_fastdiv_check_bounded",
-    "smx_tune_block", "smx_tune_block_pipe", "smx_tune_block_form", "smx_tune_block_persist", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
+    "smx_tune_block", "smx_tune_block_pipe", "smx_tune_block_pipe_cus", "smx_tune_block_form", "smx_tune_block_persist", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_graph_create",
@@ -155,6 +155,7 @@ def load():
                                      ctypes.POINTER(vp)], ctypes.c_int),
         "smx_tune_block": ([i32], ctypes.c_int),
         "smx_tune_block_pipe": ([i32], ctypes.c_int),
+        "smx_tune_block_pipe_cus": ([i32, i32], ctypes.c_int),
         "smx_tune_block_form": ([i32], ctypes.c_int),
         "smx_tune_block_persist": ([i32], ctypes.c_int),
         "smx_block_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
@@ -272,6 +273,14 @@ def tune_block_pipe(on: int = -1) -> int:
     next block on a second stream during each sweep (opt-in), -1 query only; returns the previous
     setting."""
     return int(load().smx_tune_block_pipe(on))
+
+
+def tune_block_pipe_cus(cus_per_xcd: int = -1, parts: int = -1) -> int:
+    """smx_tune_block_pipe_cus: the CU partition of pipelined chains -- the planner on
+    ``cus_per_xcd`` CUs of every XCD (0: unpartitioned, the default), the sweeps on the rest;
+    ``parts`` > 0 caps the planner's workgroups (0: blk_parts_of); -1 keeps a setting.  Returns
+    the previous cus_per_xcd (-1: out of range, nothing changed)."""
+    return int(load().smx_tune_block_pipe_cus(cus_per_xcd, parts))
 
 
 def tune_shard_xchg(mode: int = -2) -> int:

@@ -30,6 +30,9 @@ def main() -> None:
     ap.add_argument("--persist", default="0",
                     help="smx_tune_block_persist settings to compare (planner: 0 one launch per "
                          "pivot, 1 one persistent launch per block), e.g. 0,1")
+    ap.add_argument("--pipe-cus", default="0:0",
+                    help="smx_tune_block_pipe_cus settings (CUs per XCD : planner workgroup cap), "
+                         "e.g. 0:0,2:16,4:32 (with --pipe 0: the planner alone on those CUs)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -44,11 +47,14 @@ def main() -> None:
         dev = DeviceTableau(T, n, m, m, block=0)
         k = a.k
         ref_log = ref_tab = None
-        runs = [(0, 0, 0, 0)] + [(int(x), int(pp), int(f), int(ps))
-                                 for x in a.pivots.split(",") for pp in a.pipe.split(",")
-                                 for f in a.form.split(",") for ps in a.persist.split(",")]
-        for P, pipe, form, persist in runs:
+        cus = [tuple(int(v) for v in c.split(":")) for c in a.pipe_cus.split(",")]
+        runs = [(0, 0, 0, 0, (0, 0))] + [(int(x), int(pp), int(f), int(ps), cu)
+                                         for x in a.pivots.split(",") for pp in a.pipe.split(",")
+                                         for f in a.form.split(",") for ps in a.persist.split(",")
+                                         for cu in cus]
+        for P, pipe, form, persist, cu in runs:
             _lib.tune_block_pipe(pipe)
+            _lib.tune_block_pipe_cus(*cu)
             _lib.tune_block_form(form)
             _lib.tune_block_persist(persist)
             dev.close()   # captured graphs bake in the layout: capture afresh for every run
@@ -71,7 +77,7 @@ def main() -> None:
             log = dev.read_log(0, int(ctl["npivots"]))
             tab = dev.download().view(np.int64)
             row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "pipe": pipe,
-                   "form": form, "persist": persist, "k": k,
+                   "form": form, "persist": persist, "pipe_cus": list(cu), "k": k,
                    "bpc": a.bpc,
                    "us_per_pivot": ms * 1e3 / k, "pivots_s": k / ms * 1e3,
                    "npivots": int(ctl["npivots"])}
@@ -82,8 +88,11 @@ def main() -> None:
                                             np.array_equal(tab, ref_tab))
                 dev.upload(T)
                 dev.step = 0
-                sw, tot = dev.run_block_timed(k, P)
-                dev.sync_state()
+                sw, tot = dev.run_block_timed(k, P)   # eager: CU partitions apply here only
+                ctl = dev.sync_state()
+                row["eager_same_as_fused"] = bool(
+                    np.array_equal(dev.read_log(0, int(ctl["npivots"])), ref_log) and
+                    np.array_equal(dev.download().view(np.int64), ref_tab))
                 row["sweep_us"] = float(np.mean(sw)) * 1e3
                 row["sweep_gbs"] = 16.0 * N * N / (float(np.mean(sw)) * 1e-3) / 1e9
                 row["eager_us_per_pivot"] = tot * 1e3 / k
