@@ -366,8 +366,9 @@ int smx_tune_block_persist(int32_t on);
  * stream of the library while block b is swept (from block b's input table, every chain prefixed
  * by block b's pivots), the sweeps work out of place, the ragged block comes first, and a final
  * settle kernel restores the buf[(parity + d) & 1] convention when a terminal outcome cut the
- * chain.  0 plans each block on the caller's stream before its sweep.  -1 keeps the setting;
- * returns the previous one. */
+ * chain.  1: the planner's register prefix form (k_blk_step_pfx) after blocks of 12 or 20, the
+ * LDS-rolled form (k_blk_step_lag) otherwise; 2: the LDS-rolled form always (A/B).  0 plans each
+ * block on the caller's stream before its sweep.  -1 keeps the setting; returns the previous one. */
 int smx_tune_block_pipe(int32_t on);
 /* CU partition of pipelined chains (default 0, 0): cus_per_xcd > 0 runs the planner on that many
  * CUs of every XCD and the sweeps on the rest (two CU-masked library streams; the caller's stream

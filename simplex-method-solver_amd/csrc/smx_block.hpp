@@ -149,6 +149,9 @@ __host__ __device__ __forceinline__ const int32_t* blk_rflags(const double* mul,
 __host__ __device__ __forceinline__ double* blk_mulT(double* mul, int64_t R) {
     return mul + R * kBlkMax + (R * 4 + 255) / 256 * 256 / 8;
 }
+__host__ __device__ __forceinline__ const double* blk_mulT(const double* mul, int64_t R) {
+    return mul + R * kBlkMax + (R * 4 + 255) / 256 * 256 / 8;
+}
 
 __device__ __forceinline__ int32_t blk_rflag(bool piv, bool bnd, bool zero) {
     return piv ? 2 : (!bnd ? 0 : (zero ? 3 : 1));
@@ -389,6 +392,20 @@ __device__ __forceinline__ double blk_prv(const double* __restrict__ T, int64_t 
     double p[kBlkMax];
     blk_load_col<D>(pr, ld, j, p);
     return blk_chain<D>(T[(int64_t)r * ld + j], r, j, pv, p, mqr);
+}
+
+// Pipelined register form (k_blk_step_pfx): x = X_b[i][j] -> X_{b+1}[i][j] through the previous
+// block's PP pivots (pv: their r / c / e / y in LDS, p[q] = that block's pivot row q at column j,
+// mq[q] = row i's multipliers of that block), fast division with the exact recompute when the
+// wave's vote fails -- the chain prefix of blk_chain_rolled, unrolled in registers.  Either way
+// the operations of PP single-pivot sweeps, so the same bits.
+template <int PP>
+__device__ __forceinline__ double blk_pfx(double x, int i, int j, const BlkPiv& pv, bool ok,
+                                          const double* p, const double* mq) {
+    uint32_t wt = 0;
+    const double v = blk_chain_fd<PP>(x, i, j, pv, p, mq, wt);
+    if (ok && __all(wt < kWinSpan)) return v;
+    return blk_chain<PP>(x, i, j, pv, p, mq);
 }
 
 // A lane's double, read by every lane (two v_readlane_b32: the value lands in scalar registers)
@@ -758,7 +775,11 @@ __device__ unsigned g_blk_fallback[kBlkMax + 1][2];
 // hs the chain state (slot 0).  The operands the row pass shares (pivot-row values at the
 // columns it reads, row r's multipliers) sit in LDS, keeping the kernel small enough to run next
 // to a sweep.
-template <int L, bool SH, bool LAG>
+// PP > 0 (pipelined register form, unsharded): T is the previous block's input table X_b and
+// every value read from it is first taken through that block's PP pivots (blk_pfx: hp / mulp /
+// prp, plan slot slot ^ 1), so the register form's chains, caches and fused phase 2 run
+// unchanged on X_{b+1}.
+template <int L, bool SH, bool LAG, int PP = 0>
 __device__ __forceinline__ bool blk_step_body(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int row0,
     int P, int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
@@ -786,6 +807,13 @@ __device__ __forceinline__ bool blk_step_body(
     __shared__ int s_nb, s_c;
     __shared__ int64_t s_off;
     __shared__ double s_e, s_fc, s_pm, s_pa;
+    // PP > 0: the previous block's pivots (with y), its pivot rows at columns c, m, cf, and
+    // whether every one of its pivot elements is inside the fast-division window
+    constexpr int PPS = PP > 0 ? PP : 1;
+    __shared__ BlkPiv s_pvp;
+    __shared__ double s_colp[3][PPS];
+    __shared__ int s_okp;
+    static_assert(PP == 0 || (!SH && !LAG && PP <= kBlkMax), "prefix: unsharded register form");
     const int tid = threadIdx.x;
     const int b = blockIdx.x, G = gridDim.x;
     SMX_BLK_STAMP(0);
@@ -825,6 +853,20 @@ __device__ __forceinline__ bool blk_step_body(
             s_off = sd.off;
         }
     } else if (tid < kWave) {
+        if constexpr (PP > 0) {   // (issued with the records' loads: the same round trip)
+            bool okp = true;
+            if (tid < PP) {
+                const double e = hp->e[tid];
+                const FastDiv fd = fd_prep(e);
+                s_pvp.r[tid] = hp->r[tid];
+                s_pvp.c[tid] = hp->c[tid];
+                s_pvp.e[tid] = e;
+                s_pvp.y[tid] = fd.y;
+                okp = fd.ok;
+            }
+            okp = __all(okp);
+            if (tid == 0) s_okp = okp ? 1 : 0;
+        }
         // the decision of step D from its records (every workgroup, identically)
         const int c = hs->cfs[blk_slot(D, P, bn)];
         int nb;
@@ -914,8 +956,25 @@ __device__ __forceinline__ bool blk_step_body(
         }
         double x = T[(int64_t)r_local * ld + j];
         double p[kBlkMax];
-        blk_load_col<D>(pr, ld, j, p);
-        blk_pin(x);
+        if constexpr (PP > 0) {   // both chains' operands in one round trip
+            double pP[PPS], mP[PPS];
+#pragma unroll
+            for (int q = 0; q < PP; ++q) {
+                pP[q] = prp[(int64_t)q * ld + j];
+                mP[q] = mulp[(int64_t)r_local * kBlkMax + q];
+            }
+            blk_load_col<D>(pr, ld, j, p);
+#pragma unroll
+            for (int q = 0; q < PP; ++q) {
+                blk_pin(pP[q]);
+                blk_pin(mP[q]);
+            }
+            blk_pin(x);
+            x = blk_pfx<PP>(x, r_local, j, s_pvp, s_okp != 0, pP, mP);
+        } else {
+            blk_load_col<D>(pr, ld, j, p);
+            blk_pin(x);
+        }
         uint32_t wt = 0;
         const double v = blk_chain_fd<D>(x, r_local, j, pvD, p, mqr, wt);
         if (okD && __all(wt < kWinSpan)) return v;
@@ -950,10 +1009,45 @@ __device__ __forceinline__ bool blk_step_body(
 #pragma unroll
         for (int k = 0; k < NSC; ++k) jj[2 + k] = tid + k * NT;
         double x[NJ], pq[NJ][kBlkMax], fv[NJ];
+        double xr[NJ];
+        if constexpr (PP > 0) {
+            // row r of X_{b+1} at the NJ columns first (one round trip of its own: holding both
+            // chains' operands at once would double the registers of the fused phase)
+            double pP[NJ][PPS], mP[PPS];
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) {
+                const int jc = min(jj[u], C - 1);
+                xr[u] = Tr[jc];
+#pragma unroll
+                for (int q = 0; q < PP; ++q) pP[u][q] = prp[(int64_t)q * ld + jc];
+            }
+#pragma unroll
+            for (int q = 0; q < PP; ++q) mP[q] = mulp[(int64_t)r_local * kBlkMax + q];
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) {
+                blk_pin(xr[u]);
+#pragma unroll
+                for (int q = 0; q < PP; ++q) blk_pin(pP[u][q]);
+            }
+#pragma unroll
+            for (int q = 0; q < PP; ++q) blk_pin(mP[q]);
+            uint32_t wtp = 0;
+            double yr[NJ];
+#pragma unroll
+            for (int u = 0; u < NJ; ++u)
+                yr[u] = blk_chain_fd<PPS>(xr[u], r_local, jj[u], s_pvp, pP[u], mP, wtp);
+            if (!s_okp || !__all(wtp < kWinSpan)) {
+#pragma unroll
+                for (int u = 0; u < NJ; ++u)
+                    yr[u] = blk_chain<PPS>(xr[u], r_local, jj[u], s_pvp, pP[u], mP);
+            }
+#pragma unroll
+            for (int u = 0; u < NJ; ++u) xr[u] = yr[u];
+        }
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
             const int jc = min(jj[u], C - 1);
-            x[u] = Tr[jc];
+            x[u] = PP > 0 ? xr[u] : Tr[jc];
             fv[u] = fo[jc];
 #pragma unroll
             for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
@@ -1166,6 +1260,12 @@ __device__ __forceinline__ bool blk_step_body(
             s_col[1][tid] = pr[(int64_t)tid * ld + m];
             if (cf != SMX_NONE) s_col[2][tid] = pr[(int64_t)tid * ld + cf];
         }
+        if (PP > 0 && tid >= kWave && tid < kWave + PP) {   // (a wave the stores above spare)
+            const int q = tid - kWave;
+            s_colp[0][q] = prp[(int64_t)q * ld + c];
+            s_colp[1][q] = prp[(int64_t)q * ld + m];
+            if (cf != SMX_NONE) s_colp[2][q] = prp[(int64_t)q * ld + cf];
+        }
     }
     __syncthreads();
     SMX_BLK_STAMP(5);
@@ -1228,6 +1328,9 @@ __device__ __forceinline__ bool blk_step_body(
             const int n = pp + D;
             const double mc = blk_chain_rolled(xc, i, c, s_all, n, s_colall[0], op);
             mr[D] = mc;                                              // T_{k+D}[i][c]
+            // (and transposed: the next block's planner may be the prefix form, whose row pass
+            // reads this block's multipliers from blk_mulT)
+            blk_mulT(mul, rows + 1)[(int64_t)D * (rows + 1) + i] = mc;
             op[n] = mc;
             if (L == P) {   // the sweep's per-row flag (this block's multipliers, blk_rflags)
                 bool bnd = bnd_or_zero(mc), zero = (dbits(mc) << 1) == 0;
@@ -1244,12 +1347,36 @@ __device__ __forceinline__ bool blk_step_body(
         } else {
             double mq[kBlkMax];
             double x3[3] = {xc, xb, xa};
+            double mP[PPS];
 #pragma unroll
             for (int q = 0; q < D; ++q) mq[q] = mT[(int64_t)q * (rows + 1) + i];
+            if constexpr (PP > 0) {
+                const double* mTp = blk_mulT(mulp, rows + 1);
+#pragma unroll
+                for (int q = 0; q < PP; ++q) mP[q] = mTp[(int64_t)q * (rows + 1) + i];
+            }
 #pragma unroll
             for (int q = 0; q < D; ++q) blk_pin(mq[q]);
 #pragma unroll
             for (int k = 0; k < 3; ++k) blk_pin(x3[k]);
+            if constexpr (PP > 0) {
+                // the values read from X_b (not the caches) through the previous block's pivots
+#pragma unroll
+                for (int q = 0; q < PP; ++q) blk_pin(mP[q]);
+                const bool pc = !reuse_c, pb = D == 0, pa = cf != SMX_NONE;
+                uint32_t wtp = 0;
+                double y3[3] = {x3[0], x3[1], x3[2]};
+                if (pc) y3[0] = blk_chain_fd<PPS>(x3[0], i, c, s_pvp, s_colp[0], mP, wtp);
+                if (pb) y3[1] = blk_chain_fd<PPS>(x3[1], i, m, s_pvp, s_colp[1], mP, wtp);
+                if (pa) y3[2] = blk_chain_fd<PPS>(x3[2], i, cf, s_pvp, s_colp[2], mP, wtp);
+                if (!s_okp || !__all(wtp < kWinSpan)) {
+                    if (pc) y3[0] = blk_chain<PPS>(x3[0], i, c, s_pvp, s_colp[0], mP);
+                    if (pb) y3[1] = blk_chain<PPS>(x3[1], i, m, s_pvp, s_colp[1], mP);
+                    if (pa) y3[2] = blk_chain<PPS>(x3[2], i, cf, s_pvp, s_colp[2], mP);
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) x3[k] = y3[k];
+            }
             // x3[0]: T_{k+D}[i][c] itself when cached (reuse_c), else T_k[i][c]; x3[1]:
             // T_{k+D}[i][m] (cached) from step 1 on, T_k[i][m] at step 0
             constexpr int QB = D > 0 ? D : 0;
@@ -1312,6 +1439,12 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_step(SMX_BLK_STEP_PARAMS) {
 template <int L>
 __global__ __launch_bounds__(kBlkNT) void k_blk_step_lag(SMX_BLK_STEP_PARAMS) {
     blk_step_body<L, false, true>(SMX_BLK_STEP_ARGS);
+}
+// Pipelined register form: the register form on X_b with every read prefixed by the previous
+// block's PP pivots (blk_pfx); for the planner's own CUs of a partitioned chain
+template <int L, int PP>
+__global__ __launch_bounds__(kBlkNT) void k_blk_step_pfx(SMX_BLK_STEP_PARAMS) {
+    blk_step_body<L, false, false, PP>(SMX_BLK_STEP_ARGS);
 }
 
 #undef SMX_BLK_STEP_PARAMS

@@ -599,6 +599,26 @@ int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, s
     return (int)hipGetLastError();
 }
 
+// smx_tune_block_pipe: 1 plans block b+1 on a second stream while block b is swept (the
+// register prefix form k_blk_step_pfx where it is instantiated -- blocks of 12 or 20 after blocks
+// of 12 or 20 -- else the LDS-rolled k_blk_step_lag); 2 the same with k_blk_step_lag always;
+// 0 (default) plans every block on the solver stream right before its sweep.
+int g_block_pipe = 0;
+
+template <int PP, int... Is>
+BlkStepFn blk_pfx_pick(int L, std::integer_sequence<int, Is...>) {
+    static const BlkStepFn t[] = {k_blk_step_pfx<Is + 1, PP>...};
+    return t[L - 1];
+}
+// the register prefix form of step L after a block of pp pivots, or nullptr
+BlkStepFn blk_pfx_fn(int L, int pp) {
+    if (pp == 20 && L >= 1 && L <= 20)
+        return blk_pfx_pick<20>(L, std::make_integer_sequence<int, 20>{});
+    if (pp == 12 && L >= 1 && L <= 12)
+        return blk_pfx_pick<12>(L, std::make_integer_sequence<int, 12>{});
+    return nullptr;
+}
+
 // One planner launch of block bn (plan slot `slot`).  pp > 0 (pipelined chains): T is the
 // previous block's input table and that block's pp pivots (plan slot slot ^ 1) prefix every chain.
 int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, int parity,
@@ -607,6 +627,10 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
                     int pp = 0, const double* xrow = nullptr, int64_t xslot = 0) {
     BlkStepFn fn = sh ? blk_step_fn_sh<true, false>(L)
                       : (pp > 0 ? blk_step_fn_sh<false, true>(L) : blk_step_fn_sh<false, false>(L));
+    if (!sh && pp > 0 && g_block_pipe == 1) {
+        const BlkStepFn f = blk_pfx_fn(L, pp);
+        if (f) fn = f;
+    }
     const int o = slot ^ 1;
     hipLaunchKernelGGL(fn, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
                        fscan_of(s), s.row0, P, parity, bn, ctl, b.h[slot], b.h[0], b.parts,
@@ -714,9 +738,6 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     return (int)hipGetLastError();
 }
 
-// smx_tune_block_pipe: 1 plans block b+1 on a second stream while block b is swept;
-// 0 (default) plans every block on the solver stream right before its sweep.
-int g_block_pipe = 0;
 
 // smx_tune_block_pipe_cus: r > 0 gives the planner of a pipelined chain r CUs of every XCD and
 // the sweeps the other 32 - r (two CU-masked streams, hipExtStreamCreateWithCUMask), so the
@@ -1751,7 +1772,7 @@ int smx_tune_block_persist(int32_t on) {
 
 int smx_tune_block_pipe(int32_t on) {
     const int prev = g_block_pipe;
-    if (on >= 0) g_block_pipe = on ? 1 : 0;
+    if (on >= 0) g_block_pipe = on == 2 ? 2 : (on ? 1 : 0);
     return prev;
 }
 

@@ -270,8 +270,9 @@ def tune_block_form(form: int = -1) -> int:
 
 def tune_block_pipe(on: int = -1) -> int:
     """smx_tune_block_pipe: 0 plan every block on the solver stream (the default), 1 plan the
-    next block on a second stream during each sweep (opt-in), -1 query only; returns the previous
-    setting."""
+    next block on a second stream during each sweep (opt-in; the register prefix form after
+    blocks of 12 / 20), 2 the same with the LDS-rolled planner always, -1 query only; returns the
+    previous setting."""
     return int(load().smx_tune_block_pipe(on))
 
 

@@ -3,7 +3,9 @@ launch_block_chain_pipe): block b+1 is planned on a second stream from block b's
 (every chain prefixed by block b's pivots) while block b is swept out of place.  Bit-exact
 against the unpipelined block chain, the one-pivot chain and the C oracle -- pivot logs, tables,
 control blocks and the x-history ring -- for ragged-first blocks, terminal outcomes in any block
-(the settle kernel), graph replays and the timed path.
+(the settle kernel), graph replays and the timed path; both planner forms (the register prefix
+form k_blk_step_pfx after blocks of 12 / 20, the LDS-rolled k_blk_step_lag) and the CU partition
+(smx_tune_block_pipe_cus: planner and sweeps on CU-masked streams, eager chains).
 """
 from __future__ import annotations
 
@@ -26,16 +28,19 @@ def _need_gpu():
 def modes():
     """set(P, pipe) for one test (resident loop off); restores the library policies."""
     from simplex_mi355x import _lib
-    prev = (_lib.tune_block(-1), _lib.tune_block_pipe(-1), _lib.tune_resident(-2))
+    prev = (_lib.tune_block(-1), _lib.tune_block_pipe(-1), _lib.tune_resident(-2),
+            _lib.tune_block_pipe_cus(-1, -1))
     _lib.tune_resident(-1)
 
-    def set_(P, pipe):
+    def set_(P, pipe, cus=(0, 0)):
         _lib.tune_block(P)
         _lib.tune_block_pipe(pipe)
+        _lib.tune_block_pipe_cus(*cus)
     yield set_
     _lib.tune_block(prev[0])
     _lib.tune_block_pipe(prev[1])
     _lib.tune_resident(prev[2])
+    _lib.tune_block_pipe_cus(prev[3], 0)
 
 
 def _state(sm, k):
@@ -47,7 +52,7 @@ def _state(sm, k):
             sm._dev.read_xhist(0, min(k, int(c["npivots"]))).view(np.int64).tobytes())
 
 
-@pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("P", [2, 3, 5, 8, 12, 20])
 def test_pipe_equals_unpipelined_on_fixtures(modes, P):
     """Every non-capped random fixture, chunks of 3P+1 pivots (ragged first block, several
     blocks, terminal outcomes inside any of them): the pipelined chain leaves exactly the
@@ -165,3 +170,44 @@ def test_pipe_timed_run_16k_prefix_vs_oracle(modes, k):
     got = dev.download()
     assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
     assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
+
+
+# The register prefix form (pipe 1 after blocks of 12 / 20) against the LDS-rolled form (pipe 2)
+# and the C oracle, unpartitioned and on a CU partition (4 CUs per XCD, 32 planner workgroups);
+# eager chains (a partition does not survive stream capture), then a graph replay of the same.
+@pytest.mark.parametrize("kind,n,m,k,P", [
+    ("uniform", 2047, 2047, 64, 20),           # 4 + 20 + 20 + 20: the rolled form plans block 1
+    ("uniform", 1535, 1791, 72, 12),           # whole blocks: every later block in prefix form
+    ("mixed", 1023, 1023, 130, 20),            # phase 1 first
+    ("degenerate", 1023, 1023, 120, 12),       # zero pivot-row entries, exact fallbacks
+    ("degenerate_mixed", 1200, 600, 100, 20),
+    ("uniform", 65535, 255, 60, 20),           # tall: several rows per planner thread
+])
+@pytest.mark.parametrize("pipe,cus", [(1, (0, 0)), (1, (4, 32)), (2, (4, 32))])
+def test_pipe_prefix_form_vs_oracle(modes, kind, n, m, k, P, pipe, cus):
+    from oracle import c_oracle
+    from simplex_mi355x import lp
+    import simplex
+    T = lp.dense_tableau(kind, 7, n, m)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    for graph in (False, True):
+        modes(P, pipe, cus)
+        sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+        assert sm._dev.block_plan()[1] == P
+        sm.solve(record_history=False, max_pivots=k, chunk=k, graph=graph)
+        assert sm.pivots == done, (graph, sm.pivots, done, st)
+        assert sm.pivot_log == [tuple(map(int, x)) for x in log], graph
+        got = sm._dev.download()
+        assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64)), graph
+        assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64)), graph
+
+
+def test_pipe_partition_knob():
+    from simplex_mi355x import _lib
+    prev = _lib.tune_block_pipe_cus(-1, -1)
+    try:
+        assert _lib.tune_block_pipe_cus(17, 0) == -1        # out of range: unchanged
+        assert _lib.tune_block_pipe_cus(4, 32) == prev
+        assert _lib.tune_block_pipe_cus(-1, -1) == 4
+    finally:
+        _lib.tune_block_pipe_cus(prev, 0)
