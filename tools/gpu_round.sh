@@ -11,6 +11,7 @@
 #   bench20 / bench200     bench.py --steps 20 --warmup 5 (the driver's line) / --steps 200 --warmup 20
 #   benchN=ARGS            bench.py with ARGS (`benchN=--size,8192,--steps,200` -> benchN.log)
 #   stats20 / stats200     rocprofv3 --kernel-trace --stats of bench20 / bench200 (no cpu baseline)
+#   statsN=ARGS            rocprofv3 --kernel-trace --stats of bench.py ARGS (-> gpurun_out/TAG/N_statsN/)
 #   fetch20 / write20      rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench20
 #   sq20 / clock200        rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES of bench20; GRBM_GUI_ACTIVE
 #                          GRBM_COUNT SQ_INSTS_VALU SQ_BUSY_CYCLES of bench200 (the clock per sweep)
@@ -55,6 +56,7 @@ for spec in "$@"; do
     bench200) cmd="cd $R && python -u bench.py --gpus 1 --steps 200 --warmup 20 --no-cpu-baseline"; d=300 ;;
     benchN) cmd="cd $R && python -u bench.py $arg"; d=400 ;;
     stats20) cmd="cd /tmp && rocprofv3 --kernel-trace --stats -d $O/stats20 -o run --output-format csv -- $B --steps 20 --warmup 5"; d=300 ;;
+    statsN) cmd="cd /tmp && rocprofv3 --kernel-trace --stats -d $O/$tag -o run --output-format csv -- $B $arg"; d=300 ;;
     stats200) cmd="cd /tmp && rocprofv3 --kernel-trace --stats -d $O/stats200 -o run --output-format csv -- $B --steps 200 --warmup 20"; d=300 ;;
     fetch20) cmd="cd /tmp && timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $O/fetch20 -o run --output-format csv -- $B --steps 20 --warmup 5"; d=300 ;;
     write20) cmd="cd /tmp && timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $O/write20 -o run --output-format csv -- $B --steps 20 --warmup 5"; d=300 ;;

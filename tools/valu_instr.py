@@ -21,9 +21,9 @@ SUMMARIES = ["profiles/r02d/sweep8_pmc_summary.json",
              "profiles/r03/sweep10_pmc_summary.json",
              "profiles/r03c/sweep12_pmc_summary.json"]
 # (counter CSV, pivots per sweep of the dispatches to read, what the pass was)
-PASSES = [("profiles/r04u/pmc/sq20_counter_collection.csv", 20,
-           "rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES, bench.py --steps 20: one k_blk_sweep<20, 5> "
-           "launch")]
+PASSES = [("profiles/r05l/sq20/run_counter_collection.csv", 20,
+           "rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES, bench.py --steps 20 --warmup 5 (round 5): "
+           "every k_blk_sweep<20, 5> dispatch")]
 SIZE = 16384
 _SWEEP = re.compile(r"k_blk_sweep<(\d+)[,>]")
 
