@@ -1816,7 +1816,10 @@ __device__ __forceinline__ void blk_fixcols(double* out, int64_t ld, int R, int 
     // pairs ordered pivot-major (t = q R + i): a wave's lanes share q, so the pivot rows' values
     // at column c are one address per load; every operand of the chain is loaded before its
     // first step (the loop that loaded them step by step took 9-13 us per block at 16384^2 --
-    // a memory round trip per step)
+    // a memory round trip per step).  Row i's multipliers come from the transposed copy (the
+    // planner's row pass writes it for every row but the f-row, R - 1): a wave's 64 rows are
+    // then 8 lines per multiplier instead of 64.
+    const double* mT = blk_mulT(mul, R);
     const int64_t pairs = (int64_t)R * P;
     for (int64_t t = (int64_t)blockIdx.x * kUpdBlock + threadIdx.x; t < pairs;
          t += (int64_t)gridDim.x * kUpdBlock) {
@@ -1826,12 +1829,13 @@ __device__ __forceinline__ void blk_fixcols(double* out, int64_t ld, int R, int 
         for (int q2 = q + 1; q2 < P; ++q2) last = last && h->c[q2] != c;
         if (!last) continue;
         const double* mr = mul + (int64_t)i * kBlkMax;
+        const bool frow = i == R - 1;
         double mq[kBlkMax], pc[kBlkMax], eq[kBlkMax];
         int rq[kBlkMax];
 #pragma unroll
         for (int q2 = 0; q2 < kBlkMax; ++q2) {
             const bool act = q2 >= q && q2 < P;
-            mq[q2] = act ? mr[q2] : 0.0;
+            mq[q2] = act ? (frow ? mr[q2] : mT[(int64_t)q2 * R + i]) : 0.0;
             pc[q2] = (act && q2 > q) ? pr[(int64_t)q2 * ld + c] : 0.0;
             eq[q2] = act ? h->e[q2] : 1.0;
             rq[q2] = act ? h->r[q2] : -1;

@@ -559,6 +559,8 @@ __device__ __forceinline__ bool blk_pstep(const PlanArgs& a, PlanSh& S, const in
         for (int q = 0; q < NM; ++q)
             if (q == D) mD = mq[q];
         st_ag(mul + (int64_t)i * kBlkMax + D, mD);   // read as mqr should row i pivot later
+        // the transposed copy, for the sweep's pivot-column pass (blk_fixcols; after this launch)
+        blk_mulT(mul, rows + 1)[(int64_t)D * (rows + 1) + i] = mD;
         cb = bv;
         ca = av;
         if (L == P) {   // the sweep's per-row flag (blk_rflags)
