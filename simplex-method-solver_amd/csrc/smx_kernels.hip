@@ -733,7 +733,8 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
     // the flag form's pivot columns, or a block cut short by a terminal outcome (does nothing
     // otherwise)
     // one (row, pivot) pair of the pivot columns per thread where that fits (1,280 workgroups at
-    // 16384^2 and 20 pivots: one round trip instead of 2.5 in turn, 19 -> ~6 us per block)
+    // 16384^2 and 20 pivots: 19.2 -> 17.3 us per block, profiles/r05n/stats20; what remains is the
+    // pass's scattered 8-B column stores, one per row and pivot)
     const int64_t fix_wg = ((int64_t)(s.rows + 1) * P + kUpdBlock - 1) / kUpdBlock;
     const int rest_grid = (int)std::max<int64_t>(num_cus() * 2,
                                                  std::min<int64_t>(fix_wg, num_cus() * 8));
