@@ -28,7 +28,7 @@ struct SmxBool {
 //     mul[i][q] = T_{k+q}[i][c_q]           (row i's pivot-column entry before step k+q)
 // so chain(T_k[i][j], l) IS T_{k+l}[i][j], bit for bit (same operations on the same operands in
 // the same order as l single-pivot sweeps).  A chain of blocks on T_k:
-//   k_blk_prime + k_blk_first   once per chain: the f-row of T_k (`fr`), its first negative entry
+//   k_blk_start                 once per chain: the f-row of T_k (`fr`), its first negative entry
 //                               and the records of step k (first negative "-b" row and ratio
 //                               candidates on that column, the layout of la_partial);
 //   k_blk_step<L>, L = 1..P     one launch per pivot (nparts workgroups): every workgroup decides
@@ -423,45 +423,6 @@ __device__ __forceinline__ double blk_fnew(double x, double pj, int j, int c, do
     return ((j == c) ? x : (a - b)) / e;
 }
 
-// Chain start: the f-row of T into fr[parity] and its first negative entry (simplex.py:94-98).
-// Also the chain state: loc = buffer index of T, np0 = the pivot count (even for a stopped chain).
-__global__ __launch_bounds__(1024) void k_blk_prime(const double* __restrict__ T, int64_t ld,
-                                                     int rows, int m, int fscan, int parity,
-                                                     int loc, const smx_ctl* __restrict__ ctl,
-                                                     BlkHdr* __restrict__ h,
-                                                     BlkHdr* __restrict__ h1,
-                                                     double* __restrict__ fr) {
-    __shared__ int s_tmp[1024 / kWave];
-    if (threadIdx.x == 0) {
-        h->loc = loc;
-        h->np0 = ctl->npivots;
-        h1->peff = 0;
-    }
-    if (ctl->term) return;
-    const int C = m + 1;
-    const double* f = T + (int64_t)rows * ld;
-    double* fo = fr + (int64_t)parity * ld;
-    int nf = SMX_NONE;
-    // eight loads in flight per thread before their stores (one round trip per 8192 columns;
-    // the one-at-a-time loop took ~12 us at 16384 columns)
-    constexpr int U = 8;
-    for (int j0 = threadIdx.x; j0 < C; j0 += 1024 * U) {
-        double v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = j0 + u * 1024 < C ? f[j0 + u * 1024] : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int j = j0 + u * 1024;
-            if (j < C) fo[j] = v[u];
-            if (j < fscan && v[u] < 0.0 && j < nf) nf = j;
-        }
-    }
-    nf = block_min_int<1024>(nf, s_tmp);
-    if (threadIdx.x == 0) {
-        h->cfs[blk_slot(0, 1, 0)] = nf;
-        h->peff = 0;
-    }
-}
 
 // Workgroup partial of the records (first negative "-b" row; first ratio candidate and best key)
 struct BlkRec {
@@ -577,24 +538,62 @@ __device__ __forceinline__ void blk_merge_records(const smx_part* __restrict__ s
     bb = wave_best_dpp(b);
 }
 
-// Records of a chain's first step, straight from T (workgroup b of nparts: local rows b*NT + tid
-// + q*nparts*NT, the layout of la_partial; global row indices row0 + i in the records).
-__global__ __launch_bounds__(kBlkNT) void k_blk_first(const double* __restrict__ T, int64_t ld,
-                                                      int rows, int m, int row0,
+// Chain start, one launch (round 5: k_blk_prime, one 1024-thread workgroup for the f-row, then
+// k_blk_first for the records -- 9.8 + 6.7 us and a launch gap at 16384^2): every workgroup finds
+// the f-row's first negative entry j < fscan itself (simplex.py:94-98; rounds of 4 kBlkNT
+// columns with early exit -- the same minimum in every workgroup), copies its slice of the f-row
+// into fr[parity], and builds its record of step 0 on that column (workgroup b of G: local rows
+// b*NT + tid + q*G*NT, global row indices row0 + i); workgroup 0 writes the chain state (loc =
+// buffer index of T, np0 = the pivot count, even for a stopped chain).
+__global__ __launch_bounds__(kBlkNT) void k_blk_start(const double* __restrict__ T, int64_t ld,
+                                                      int rows, int m, int fscan, int parity,
+                                                      int loc, int row0,
                                                       const smx_ctl* __restrict__ ctl,
-                                                      const BlkHdr* __restrict__ h,
+                                                      BlkHdr* __restrict__ h,
+                                                      BlkHdr* __restrict__ h1,
+                                                      double* __restrict__ fr,
                                                       smx_part* __restrict__ parts) {
+    __shared__ int s_tmp[kBlkNT / kWave];
+    const int b = blockIdx.x, G = gridDim.x, tid = threadIdx.x;
+    if (b == 0 && tid == 0) {
+        h->loc = loc;
+        h->np0 = ctl->npivots;
+        h1->peff = 0;
+    }
     if (ctl->term) return;
-    const int cf = h->cfs[blk_slot(0, 1, 0)];
-    const int b = blockIdx.x, nparts = gridDim.x;
+    const int C = m + 1;
+    const double* f = T + (int64_t)rows * ld;
+    double* fo = fr + (int64_t)parity * ld;
+    const int S = (C + G - 1) / G;
+    for (int j = b * S + tid; j < min(C, (b + 1) * S); j += kBlkNT) fo[j] = f[j];
+    int cf = SMX_NONE;
+    for (int j0 = 0; j0 < fscan && cf == SMX_NONE; j0 += 4 * kBlkNT) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kBlkNT + tid;
+            v[u] = j < fscan ? f[j] : 0.0;
+        }
+        int mn = SMX_NONE;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u * kBlkNT + tid;
+            if (j < fscan && v[u] < 0.0 && j < mn) mn = j;
+        }
+        cf = block_min_int_dpp<kBlkNT>(mn, s_tmp);
+    }
+    if (b == 0 && tid == 0) {
+        h->cfs[blk_slot(0, 1, 0)] = cf;
+        h->peff = 0;
+    }
     BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
-    for (int i = b * kBlkNT + (int)threadIdx.x; i < rows; i += nparts * kBlkNT) {
+    for (int i = b * kBlkNT + tid; i < rows; i += G * kBlkNT) {
         const double* row = T + (int64_t)i * ld;
         const double bv = row[m];
         const double a = cf != SMX_NONE ? row[cf] : 0.0;
         blk_rec_add(R, row0 + i, bv, cf != SMX_NONE, a);
     }
-    blk_rec_store(R, parts + (int64_t)blk_slot(0, 1, 0) * nparts + b);
+    blk_rec_store(R, parts + (int64_t)blk_slot(0, 1, 0) * G + b);
 }
 
 __device__ __forceinline__ void blk_load_pivots(const BlkHdr* __restrict__ h, int D, BlkPiv* s_pv) {
@@ -1274,8 +1273,8 @@ __device__ __forceinline__ bool blk_step_body(
     const int hl0 = hx0 >= row0 && hx0 < row0 + rows ? hx0 - row0 : -1;
     const int hl1 = hx1 >= row0 && hx1 < row0 + rows ? hx1 - row0 : -1;
     // Column cache: a column read over all rows is one 8-byte load per row, a DRAM page apart
-    // each, and such reads are most of a step's time (k_blk_first, two of them per row, takes
-    // ~8 us at 16384 rows).  Within a block the base table is fixed, so its "-b" column is read
+    // each, and such reads are most of a step's time (round 4's k_blk_first, two of them per
+    // row, took ~8 us at 16384 rows).  Within a block the base table is fixed, so its "-b" column is read
     // once (step 0) and the column the next step's records are built on -- the next entering
     // column in phase 2 -- is kept from the step that read it: one strided column per step
     // instead of three.

@@ -592,10 +592,9 @@ BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
 // loc: buffer index (0/1) of T
 int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, smx_ctl* ctl,
                      const BlkPtrs& b, hipStream_t st) {
-    hipLaunchKernelGGL(k_blk_prime, dim3(1), dim3(1024), 0, st, T, s.ld, s.rows, s.m,
-                       fscan_of(s), parity, loc, (const smx_ctl*)ctl, b.h[0], b.h[1], b.fr);
-    hipLaunchKernelGGL(k_blk_first, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
-                       s.row0, (const smx_ctl*)ctl, (const BlkHdr*)b.h[0], b.parts);
+    hipLaunchKernelGGL(k_blk_start, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
+                       fscan_of(s), parity, loc, s.row0, (const smx_ctl*)ctl, b.h[0], b.h[1],
+                       b.fr, b.parts);
     return (int)hipGetLastError();
 }
 
