@@ -386,8 +386,8 @@ def run_single(args):
             extra["two_term"] = two_term(R, C, args.steps / len(sw), instr, avg_kernel,
                                          bytes_per_sweep)
         # every launch of the chain: k_blk_start, per block Pb k_blk_step and k_blk_sweep +
-        # k_blk_sweep_rest, k_blk_publish
-        kernels_per_pivot = (args.steps + 2 * len(sw) + 2) / args.steps
+        # k_blk_sweep_rest (the last one also publishes the chain's state)
+        kernels_per_pivot = (args.steps + 2 * len(sw) + 1) / args.steps
     else:
         # the timed region replays one pre-captured hipGraph of K chained pivots (one fused
         # k_update per pivot, or the LDS-resident loop for tableaux that fit on chip); HIP events

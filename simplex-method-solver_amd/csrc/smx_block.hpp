@@ -1881,19 +1881,44 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep(double* b_in, double* b
     blk_sweep_body_flag<P, FORM>(b_in, out, ld, R, C, h, pr, mul);
 }
 
+// End of a block chain: the state of the final table into ctl slot `parity` (first negative
+// "-b" row from the records, first negative f-row entry from the chain state); one full wave.
+__device__ __forceinline__ void blk_publish_wave(const BlkHdr* __restrict__ h,
+                                                 const smx_part* __restrict__ parts, int nparts,
+                                                 int slot, int parity, smx_ctl* __restrict__ ctl) {
+    if (ctl->term) return;
+    const smx_part* sp = parts + (int64_t)slot * nparts;
+    int nb = SMX_NONE;
+    for (int k = threadIdx.x; k < nparts; k += kWave) nb = min(nb, sp[k].p1col);
+    nb = wave_min_int_dpp(nb);
+    if (threadIdx.x == 0) {
+        ctl->negb[parity] = nb;
+        ctl->negf[parity] = h->cfs[slot];
+        ctl->negb[parity ^ 1] = SMX_NONE;
+        ctl->negf[parity ^ 1] = SMX_NONE;
+    }
+}
+
 // After k_blk_sweep<P> (one launch, whichever case holds):
 // * fix = 1 and the block applied all P pivots (flag form): blk_fixcols, the pivot columns;
 // * a block that stopped early (a terminal outcome after 0 < peff < P pivots; once per LP):
 //   every element through the peff pivots with the exact division, a rolled loop reading each
 //   pivot's operands as it goes -- one small kernel for every count instead of a body per count;
 // * otherwise nothing.
+// * pctl != nullptr (the chain's last block): workgroup 0's first wave also publishes the chain's
+//   final state (k_blk_publish's work, one launch and its gap fewer per chain).
 __global__ __launch_bounds__(kUpdBlock) void k_blk_sweep_rest(double* b_in, double* b_other,
                                                               int64_t ld, int R, int C, int P,
                                                               const BlkHdr* __restrict__ h,
                                                               const double* __restrict__ mul,
                                                               const double* __restrict__ pr,
                                                               BlkHdr* __restrict__ hs, int ipx,
-                                                              int in_idx, int fix, int ipx_full) {
+                                                              int in_idx, int fix, int ipx_full,
+                                                              const smx_part* __restrict__ pparts,
+                                                              int pnparts, int pslot, int pparity,
+                                                              smx_ctl* __restrict__ pctl) {
+    if (pctl != nullptr && blockIdx.x == 0 && threadIdx.x < kWave)
+        blk_publish_wave(hs, pparts, pnparts, pslot, pparity, pctl);
     const int peff = h->peff;
     if (peff == P && fix) {
         double* out = (ipx_full >= 0 && ((ipx_full + P) & 1) == 0) ? b_in : b_other;
@@ -1937,17 +1962,7 @@ __global__ __launch_bounds__(kWave) void k_blk_publish(const BlkHdr* __restrict_
                                                        const smx_part* __restrict__ parts,
                                                        int nparts, int slot, int parity,
                                                        smx_ctl* __restrict__ ctl) {
-    if (ctl->term) return;
-    const smx_part* sp = parts + (int64_t)slot * nparts;
-    int nb = SMX_NONE;
-    for (int k = threadIdx.x; k < nparts; k += kWave) nb = min(nb, sp[k].p1col);
-    nb = wave_min_int_dpp(nb);
-    if (threadIdx.x == 0) {
-        ctl->negb[parity] = nb;
-        ctl->negf[parity] = h->cfs[slot];
-        ctl->negb[parity ^ 1] = SMX_NONE;
-        ctl->negf[parity ^ 1] = SMX_NONE;
-    }
+    blk_publish_wave(h, parts, nparts, slot, parity, ctl);
 }
 
 // End of a pipelined chain: the table after the d pivots it applied belongs in

@@ -701,10 +701,13 @@ int sweep_grid_lds(const smx_shape& s, int bpc) {
 }
 
 // ipx / in_idx: see blk_out (ipx 0: in place when the pivots applied are even, the layout of the
-// unpipelined chains; -1: never in place); plan slot `slot`.
+// unpipelined chains; -1: never in place); plan slot `slot`.  pub_ctl (the chain's last block):
+// the pivot-column pass also publishes the chain's final state (block pub_bn's first records,
+// parity pub_parity) -- k_blk_publish's work without its launch.
 int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, char* blk,
                        const BlkLayout& L, hipStream_t st, int slot = 0, int ipx = 0,
-                       int in_idx = 0, int ipx_part = 0) {
+                       int in_idx = 0, int ipx_part = 0, smx_ctl* pub_ctl = nullptr,
+                       int pub_bn = 0, int pub_parity = 0) {
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
     int form = g_block_form == 4 || g_block_form == 5 ? g_block_form
                                                       : (P > kSweepRegMaxP ? 5 : 4);
@@ -739,7 +742,8 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
                                                  std::min<int64_t>(fix_wg, num_cus() * 8));
     hipLaunchKernelGGL(k_blk_sweep_rest, dim3(rest_grid), dim3(kUpdBlock), 0, st, tin,
                        tother, s.ld, s.rows + 1, s.m + 1, P, h, mul, pr, hs, ipx_part, in_idx, 1,
-                       ipx);
+                       ipx, reinterpret_cast<const smx_part*>(blk + L.parts), blk_G(s),
+                       blk_slot(0, 1, pub_bn), pub_parity, pub_ctl);
     return (int)hipGetLastError();
 }
 
@@ -924,14 +928,17 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
             if (!err) err = (int)hipStreamWaitEvent(st, sqp->plan[0], 0);
         }
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
-        if (!err) err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st, 0, 0, p);
+        const bool lastb = done + Pb >= k;   // its pivot-column pass publishes the chain
+        if (!err)
+            err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st, 0, 0, p, 0,
+                                     lastb ? ctl : nullptr, bn + 1, (p + Pb) & 1);
         if (ev) (void)hipEventRecord(ev[2 * bn + 1], st);
         p = (p + Pb) & 1;
         done += Pb;
         ++bn;
     }
     if (err) return err;
-    return launch_blk_publish(s, p, bn, ctl, bp, st);
+    return bn == 0 ? launch_blk_publish(s, p, bn, ctl, bp, st) : 0;   // (k = 0: no block)
 }
 
 // ---- pipelined block chains (unsharded) ------------------------------------------------------
@@ -986,7 +993,8 @@ int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int 
         if (ev) hip(hipEventRecord(ev[2 * b], S));
         if (!err)
             err = launch_block_sweep(buf(in_idx), buf(in_idx ^ 1), s, Pb, blk, bp.L, S, b & 1,
-                                     last ? x : -1, in_idx, x);
+                                     last ? x : -1, in_idx, x, last ? ctl : nullptr, nb,
+                                     (parity + k) & 1);
         if (ev) hip(hipEventRecord(ev[2 * b + 1], S));
         if (!last) {
             hip(hipEventRecord(pp->sweep[b & 1], S));
@@ -999,7 +1007,6 @@ int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int 
         }
         db += Pb;
     }
-    if (!err) err = launch_blk_publish(s, (parity + k) & 1, nb, ctl, bp, S);
     if (!err)
         hipLaunchKernelGGL(k_blk_settle, dim3(num_cus() * 4), dim3(kUpdBlock), 0, S, buf0, buf1,
                            (int64_t)(s.rows + 1) * s.ld, parity, (const smx_ctl*)ctl,
