@@ -412,3 +412,31 @@ def test_persistent_graph_replays_and_tall_fallback(block_mode, planner_form):
     assert sm.pivot_log == [tuple(map(int, x)) for x in log]
     got = sm._dev.download()
     assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+
+
+@pytest.mark.parametrize("kind", ["uniform", "mixed"])
+def test_zero_pivot_chain_publishes_state(block_mode, kind):
+    """smx_block_run with k = 0: the chain start (k_blk_start) and the publish alone (no block,
+    so no pivot-column pass to carry it) -- ctl's negb / negf of the parity slot are the table's
+    first negative "-b" row and f-row column (simplex.py:72-76, :94-98), the table untouched."""
+    import torch
+    from simplex_mi355x import _lib, lp, ops
+    from simplex_mi355x.device import DeviceTableau
+    block_mode(8)
+    n, m = 3000, 2000
+    T = lp.dense_tableau(kind, 9, n, m)
+    dev = DeviceTableau(T, n, m, m)
+    plan = dev.block_plan()
+    assert plan is not None and plan[1] == 8
+    blk = dev._blk_for(plan)
+    with torch.cuda.stream(dev.stream):
+        ops.block_run(dev.buf, dev.ctl, blk, dev.log, dev.xhist, dev.shape, 0, 0, plan[1])
+    torch.cuda.synchronize()
+    c = dev.read_ctl()
+    neg_b = np.nonzero(T[:n, m] < 0.0)[0]
+    neg_f = np.nonzero(T[n, :m] < 0.0)[0]
+    assert int(c["negb"][0]) == (int(neg_b[0]) if len(neg_b) else _lib.NONE)
+    assert int(c["negf"][0]) == (int(neg_f[0]) if len(neg_f) else _lib.NONE)
+    assert int(c["npivots"]) == 0 and int(c["term"]) == 0
+    assert np.array_equal(dev.download()[:n + 1, :m + 1].view(np.int64),
+                          T[:n + 1, :m + 1].view(np.int64))
