@@ -1093,9 +1093,12 @@ int smx_timer_reserve(int32_t events) {
                       : (timer_events((size_t)events, &ev) ? (int)hipErrorOutOfMemory : 0);
 }
 
+#ifndef SMX_SRC_HASH
+#define SMX_SRC_HASH "unstamped"
+#endif
 int smx_version(char* buf, int len) {
-    const char* v = "smx 0.1 gfx950 fp64 (select, finalize, update<single|shard|forced>, reset, "
-                    "pack, merge)";
+    // "src=" + the source stamp of csrc/Makefile (SRC_HASH), checked by simplex_mi355x/_lib.py
+    const char* v = "smx 0.2 gfx950 fp64 src=" SMX_SRC_HASH;
     if (buf && len > 0) {
         strncpy(buf, v, (size_t)len - 1);
         buf[len - 1] = 0;

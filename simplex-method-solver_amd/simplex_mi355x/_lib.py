@@ -57,6 +57,50 @@ ERR_COMMS_ABORTED = -2000   # smx_mshard_run: a rank failed, every communicator 
 
 _lib = None
 
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "smx.h")
+
+
+def source_stamp() -> str | None:
+    """The stamp csrc/Makefile compiles into the library (SRC_HASH): the first 16 hex digits of
+    the SHA-256 of include/smx.h, csrc/*.hpp in name order and csrc/smx_kernels.hip, concatenated;
+    None where the sources are not next to the package."""
+    import glob
+    import hashlib
+    kern = os.path.join(CSRC, "smx_kernels.hip")
+    if not (os.path.exists(kern) and os.path.exists(INCLUDE_H)):
+        return None
+    files = [INCLUDE_H] + sorted(glob.glob(os.path.join(CSRC, "*.hpp"))) + [kern]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def library_stamp(L) -> str | None:
+    buf = ctypes.create_string_buffer(256)
+    L.smx_version(buf, 256)
+    v = buf.value.decode()
+    return v.split("src=", 1)[1].split()[0] if "src=" in v else None
+
+
+def check_stamp(L, path: str) -> None:
+    """Refuse a libsmx build whose source stamp differs from the sources in this tree (the
+    product and the diagnostic build share the stamp; other SMX_LIB builds -- A/B variants built
+    from edited sources on purpose -- are not checked)."""
+    if os.path.basename(path) not in ("libsmx.so", "libsmx_diag.so"):
+        return
+    want = source_stamp()
+    if want is None:
+        return
+    got = library_stamp(L)
+    if got != want:
+        raise OSError(f"{path} is stale: built from sources stamped {got!r}, the tree's sources "
+                      f"are {want!r}; rebuild it (`make -C simplex-method-solver_amd/csrc` or "
+                      "__graft_entry__.build())")
+
+
 EXPORTS = (
     "smx_version", "smx_nparts_for", "smx_tune_set", "smx_tune_get", "smx_tune_fused",
     "smx_set_xpos", "smx_reset", "smx_select", "smx_finalize", "smx_update",
@@ -93,6 +137,9 @@ def load():
         raise OSError(f"{LIB_PATH} not built: run `make -C simplex-method-solver_amd/csrc` "
                       "(or __graft_entry__.build()); the engine has no CPU fallback")
     L = ctypes.CDLL(LIB_PATH)
+    L.smx_version.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.smx_version.restype = ctypes.c_int
+    check_stamp(L, LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sp = ctypes.POINTER(Shape)
     sig = {

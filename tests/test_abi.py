@@ -39,6 +39,24 @@ def test_library_is_gfx950_code_object():
     assert "gfx950" in _lib.version()
 
 
+def test_library_stamp_matches_sources():
+    """The library carries the stamp of the sources it was built from (csrc/Makefile SRC_HASH) and
+    the loader refuses a stale one (the box must run what HEAD builds)."""
+    from simplex_mi355x import _lib
+    L = _lib.load()
+    assert _lib.source_stamp() is not None
+    assert _lib.library_stamp(L) == _lib.source_stamp()
+
+
+def test_stale_library_is_refused(monkeypatch):
+    from simplex_mi355x import _lib
+    L = _lib.load()
+    monkeypatch.setattr(_lib, "source_stamp", lambda: "0000000000000000")
+    with pytest.raises(OSError, match="stale"):
+        _lib.check_stamp(L, _lib.LIB_PATH)
+    _lib.check_stamp(L, "/elsewhere/libsmx_ab_variant.so")   # an A/B build is not checked
+
+
 def test_struct_layouts_match_header():
     from simplex_mi355x import _lib
     assert ctypes.sizeof(_lib.Shape) == 32
