@@ -347,37 +347,23 @@ int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear);
  * Unsharded tableaux only (row0 = 0, rows = n).  `blk` is device scratch of smx_block_bytes
  * bytes (no initialisation needed).  smx_block_bytes: with *pivots_inout = 0 it asks the
  * library's policy (smx_tune_block: 0 automatic = 10 pivots for tables of 48..256 MiB, 12 from
- * 256 MiB, 20 for 1..4 GiB, 12 beyond; 1 never, 2..24 that many) and returns 0 when chains of
+ * 256 MiB, 20 from 1 GiB; 1 never, 2..24 that many) and returns 0 when chains of
  * `shape` would not use blocks; with 1..24 it asks for that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
  * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
  * entries) and the chain's total. */
 int smx_tune_block(int32_t pivots);
+/* Planner of unsharded block chains: 0 (default) the window planner -- T_{k+D} at the first
+ * nwin - 1 columns and the "-b" column of every row, kept current pivot by pivot, one launch per
+ * pivot over up to 256 workgroups, the pivot rows at every column once per block (k_blk_wstep,
+ * k_blk_prows; columns outside the window through chains from the block's input table); 1 the
+ * register-form chains (k_blk_step).  nwin: window slots 2..64 (0 = 64, the default; -1 keeps
+ * it).  Same decisions and bits either way.  Returns the previous planner. */
+int smx_tune_block_planner(int32_t planner, int32_t nwin);
 /* Layout of the block sweep (k_blk_sweep, csrc/smx_block.hpp): 0 automatic (the default: pivot-
  * row slices in registers up to 12 pivots per sweep, in LDS shared by a workgroup's waves beyond,
  * and wherever the register layout's grid cannot give every wave one column chunk), 4 registers,
  * 5 LDS; any other value keeps the setting.  Returns the previous one.  Same bits either way. */
 int smx_tune_block_form(int32_t form);
-/* Persistent planner (csrc/smx_plan.hpp): 1 = every block of an unsharded chain is planned by ONE
- * launch (k_blk_plan: its workgroups stay resident for the block's P steps and hand each step's
- * records to the next through tagged granules), 0 = one launch per pivot (k_blk_step); -1 queries.
- * Same decisions and bits either way.  Returns the previous setting. */
-int smx_tune_block_persist(int32_t on);
-/* Pipelined block chains (default 0): with more than one block, block b+1 is planned on a second
- * stream of the library while block b is swept (from block b's input table, every chain prefixed
- * by block b's pivots), the sweeps work out of place, the ragged block comes first, and a final
- * settle kernel restores the buf[(parity + d) & 1] convention when a terminal outcome cut the
- * chain.  1: the planner's register prefix form (k_blk_step_pfx) after blocks of 12 or 20, the
- * LDS-rolled form (k_blk_step_lag) otherwise; 2: the LDS-rolled form always (A/B).  0 plans each
- * block on the caller's stream before its sweep.  -1 keeps the setting; returns the previous one. */
-int smx_tune_block_pipe(int32_t on);
-/* CU partition of pipelined chains (default 0, 0): cus_per_xcd > 0 runs the planner on that many
- * CUs of every XCD and the sweeps on the rest (two CU-masked library streams; the caller's stream
- * forks to the sweep stream and joins it at the end of the chain), so the planner neither waits
- * for a sweep's waves nor shares their CUs; parts > 0 caps the planner's workgroups so they fit
- * on its CUs.  MI355X only (256 CUs); a chain enqueued under stream capture runs unpartitioned
- * (graph kernel nodes do not keep a stream's CU mask).  -1 keeps a setting; returns the previous
- * cus_per_xcd, or -1 for an out-of-range value (nothing changed). */
-int smx_tune_block_pipe_cus(int32_t cus_per_xcd, int32_t parts);
 int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout);
 int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,
                   int32_t pivots, smx_ctl* ctl, void* blk, int64_t blk_bytes, int32_t* log,

@@ -49,13 +49,6 @@ struct SmxBool {
 // block's T_k), so a block is P + 1 launches.  A terminal outcome at step D latches ctl->term;
 // the sweep still applies the D pivots decided before it and every later kernel does nothing.
 //
-// Pipelined chains (LAG): block b+1 is planned WHILE block b is swept, on a second stream, from
-// block b's input table X_b (which that sweep only reads: the sweeps of a pipelined chain work
-// out of place) -- every chain is then prefixed by block b's pp pivots (its plan, kept in the
-// other of two plan slots), so the chain of a value of T_{k_{b+1}+D} has length pp + D.  The
-// planner leaves the critical path: a block costs one sweep instead of one sweep + P planner
-// launches.  Where the final table lands then depends on the blocks actually swept; a last
-// k_blk_settle moves it to buf[(parity + d) & 1] when a terminal outcome cut the chain.
 constexpr int kBlkMax = 24;          // pivots per block (mul row stride)
 constexpr int kBlkSlots = kBlkMax + 2;   // record / cf slots: steps 1..P-1, and two for step 0
 // Planner workgroups: four waves, one per select partial.  (Tried: one-wave workgroups, four per
@@ -79,8 +72,8 @@ __host__ __device__ __forceinline__ int blk_parts_of(int nparts, int rows) {
     return g < kBlkPartsMax ? g : kBlkPartsMax;
 }
 
-// One per plan slot (a pipelined chain alternates two); cfs / loc / np0 are the chain's state and
-// live in slot 0 only (`hs` in the kernels).
+// The block's plan (slot 0; slot 1's header only carries a zero peff); cfs / loc / np0 are the
+// chain's state.
 struct BlkHdr {
     int32_t peff;                    // pivots of this block decided so far (the sweep's count)
     int32_t pad0;
@@ -90,8 +83,6 @@ struct BlkHdr {
     int32_t loc;                     // buffer index (0/1) of the newest table a sweep wrote
     double e[kBlkMax], y[kBlkMax];   // pivot element and its refined reciprocal (fd_prep)
     int64_t np0;                     // ctl->npivots when the chain started
-    uint32_t pepoch;                 // persistent planner (smx_plan.hpp): launches so far, the
-                                     // tag epoch of its record granules (slot 0 only)
 };
 constexpr int64_t kBlkHdrBytes = 1024;   // one plan slot's header
 static_assert(sizeof(BlkHdr) <= kBlkHdrBytes, "block header");
@@ -103,29 +94,32 @@ __host__ __device__ __forceinline__ int blk_slot(int l, int P, int bn) {
     return l == 0 ? kBlkMax + (bn & 1) : (l == P ? kBlkMax + ((bn + 1) & 1) : l);
 }
 
-// Scratch layout (byte offsets; smx_block_bytes): header [2] | records [kBlkSlots][nparts] |
-// mul [2][R][kBlkMax] | pr [2][kBlkMax][ld] | fr [2][ld] (the f-row by step parity) | the
-// planner's column cache (blk_step_body).  The second header / mul / pr (plan slot 1) is used by
-// pipelined chains only.
+// Window planner (smx_window.hpp): slots per row of its [2][R][kWin] window of the first columns
+constexpr int kWin = 64;
+
+// Scratch layout (byte offsets; smx_block_bytes): header [2] | records [kBlkSlots][kBlkPartsMax] |
+// mul [2][R][kBlkMax] | pr [2][kBlkMax][ld] | fr [2][ld] (the register-form planner's f-row by step
+// parity) | the register-form planner's column caches | the window planner's window.  Plan slot 1
+// of mul / pr is unused since the pipelined planner left (kept: the layout stays put).
 struct BlkLayout {
-    int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, xr;
+    int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, win;
 };
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
+    (void)nparts;   // records sized for the widest planner (the window planner: up to 256)
     BlkLayout L;
     L.parts = 2 * kBlkHdrBytes;
-    L.mul = blk_align(L.parts + (int64_t)kBlkSlots * nparts * 32);
+    L.mul = blk_align(L.parts + (int64_t)kBlkSlots * kBlkPartsMax * 32);
     // a plan slot's multipliers [R][kBlkMax], then the sweep's per-row flags int32[R] (blk_rflags),
     // then the same multipliers transposed, [kBlkMax][R] (blk_mulT: the planner's row pass)
     L.mul_slot = blk_align(R * kBlkMax * 8 + blk_align(R * 4) + R * kBlkMax * 8);
     L.pr = L.mul + 2 * L.mul_slot;
     L.pr_slot = blk_align((int64_t)kBlkMax * ld * 8);
     L.fr = L.pr + 2 * L.pr_slot;
-    // then the planner's column caches: [R] "-b" column and [2][R] the next records' column of
-    // T_k (pipelined form), [2][R] T_{k+L}[i][cf] and [2][R] T_{k+L}[i][m] (register form)
-    // then the persistent planner's record granules: [2 step parities][kBlkPartsMax][8] uint64
-    L.xr = blk_align(L.fr + 2 * ld * 8 + 7 * R * 8);
-    L.bytes = blk_align(L.xr + (int64_t)2 * kBlkPartsMax * 8 * 8);
+    // then the register form's column caches (7 R doubles: unused [3][R], [2][R] T_{k+L}[i][cf],
+    // [2][R] T_{k+L}[i][m]), then the window [2][R][kWin] (R = rows + 1: the f-row's too)
+    L.win = blk_align(L.fr + 2 * ld * 8 + 7 * R * 8);
+    L.bytes = blk_align(L.win + (int64_t)2 * R * kWin * 8);
     return L;
 }
 
@@ -315,31 +309,6 @@ __device__ __forceinline__ double blk_chain(double x, int i, int j, const BlkPiv
     return x;
 }
 
-// Pipelined chains: the previous block's pp pivots, then this block's, as one list of at most
-// 2 * kBlkMax + 1 steps, evaluated by a rolled loop with its operands in LDS (p[q]: pivot-row
-// values at column j, mq[q]: row i's multipliers) -- the same operations in the same order as
-// blk_chain, in a few registers.
-struct BlkPiv2 {
-    int r[2 * kBlkMax + 1], c[2 * kBlkMax + 1];
-    double e[2 * kBlkMax + 1];
-};
-
-__device__ __forceinline__ double blk_chain_rolled(double x, int i, int j, const BlkPiv2& pv,
-                                                   int n, const double* p, const double* mq) {
-#pragma unroll 1
-    for (int q = 0; q < n; ++q) {
-        const double e = pv.e[q];
-        // branch-free (the row and column tests differ across lanes): both numerators, then
-        // a select -- the pivot row's products are computed and discarded
-        const double a = x * e;
-        const double b = p[q] * mq[q];
-        const bool jc = j == pv.c[q];
-        const double num = (i == pv.r[q]) ? (jc ? 1.0 : -x) : (jc ? x : (a - b));
-        x = num / e;
-    }
-    return x;
-}
-
 // A chain's operands must all be in registers before its first step: left to itself the
 // compiler sinks each load next to its use, and a chain of L steps then waits for L memory round
 // trips one after the other (the planner's scans and row pass grew by ~0.5 us per chain step,
@@ -392,20 +361,6 @@ __device__ __forceinline__ double blk_prv(const double* __restrict__ T, int64_t 
     double p[kBlkMax];
     blk_load_col<D>(pr, ld, j, p);
     return blk_chain<D>(T[(int64_t)r * ld + j], r, j, pv, p, mqr);
-}
-
-// Pipelined register form (k_blk_step_pfx): x = X_b[i][j] -> X_{b+1}[i][j] through the previous
-// block's PP pivots (pv: their r / c / e / y in LDS, p[q] = that block's pivot row q at column j,
-// mq[q] = row i's multipliers of that block), fast division with the exact recompute when the
-// wave's vote fails -- the chain prefix of blk_chain_rolled, unrolled in registers.  Either way
-// the operations of PP single-pivot sweeps, so the same bits.
-template <int PP>
-__device__ __forceinline__ double blk_pfx(double x, int i, int j, const BlkPiv& pv, bool ok,
-                                          const double* p, const double* mq) {
-    uint32_t wt = 0;
-    const double v = blk_chain_fd<PP>(x, i, j, pv, p, mq, wt);
-    if (ok && __all(wt < kWinSpan)) return v;
-    return blk_chain<PP>(x, i, j, pv, p, mq);
 }
 
 // A lane's double, read by every lane (two v_readlane_b32: the value lands in scalar registers)
@@ -552,7 +507,8 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_start(const double* __restrict__
                                                       BlkHdr* __restrict__ h,
                                                       BlkHdr* __restrict__ h1,
                                                       double* __restrict__ fr,
-                                                      smx_part* __restrict__ parts) {
+                                                      smx_part* __restrict__ parts,
+                                                      double* __restrict__ win, int nwin) {
     __shared__ int s_tmp[kBlkNT / kWave];
     const int b = blockIdx.x, G = gridDim.x, tid = threadIdx.x;
     if (b == 0 && tid == 0) {
@@ -561,6 +517,17 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_start(const double* __restrict__
         h1->peff = 0;
     }
     if (ctl->term) return;
+    // the window planner's window of T (slot `parity`; win_fill, smx_window.hpp)
+    if (win) {
+        const int lane = tid & (kWave - 1);
+        const int jl = lane < nwin ? (m + 1 <= nwin ? (lane <= m ? lane : -1)
+                                                    : (lane < nwin - 1 ? lane : m))
+                                   : -1;
+        double* Wp = win + (int64_t)parity * (rows + 1) * kWin;
+        const int nw = G * (kBlkNT / kWave);
+        for (int i = b * (kBlkNT / kWave) + (tid >> 6); i <= rows; i += nw)
+            if (jl >= 0) Wp[(int64_t)i * kWin + lane] = T[(int64_t)i * ld + jl];
+    }
     const int C = m + 1;
     const double* f = T + (int64_t)rows * ld;
     double* fo = fr + (int64_t)parity * ld;
@@ -769,75 +736,35 @@ __device__ unsigned g_blk_fallback[kBlkMax + 1][2];
 // fly; SH = true (row-sharded): from the P gathered send slots in `recv` (merge_headers), the
 // pivot row taken from the winning slot.  Pivot rows are LOCAL indices in the header (-1 when
 // another rank owns the row); the log and the labels use global ones.
-// LAG (pipelined chains, unsharded): T is the PREVIOUS block's input table and every chain starts
-// with that block's pp pivots (plan slot hp / mulp / prp); h / mul / pr are this block's slot and
-// hs the chain state (slot 0).  The operands the row pass shares (pivot-row values at the
-// columns it reads, row r's multipliers) sit in LDS, keeping the kernel small enough to run next
-// to a sweep.
-// PP > 0 (pipelined register form, unsharded): T is the previous block's input table X_b and
-// every value read from it is first taken through that block's PP pivots (blk_pfx: hp / mulp /
-// prp, plan slot slot ^ 1), so the register form's chains, caches and fused phase 2 run
-// unchanged on X_{b+1}.
-template <int L, bool SH, bool LAG, int PP = 0>
+template <int L, bool SH>
 __device__ __forceinline__ bool blk_step_body(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int row0,
     int P, int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
-    BlkHdr* __restrict__ hs, smx_part* __restrict__ parts, double* __restrict__ mul,
-    double* __restrict__ pr, double* __restrict__ fr, const double* __restrict__ recv,
-    int nranks, int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,
-    const BlkHdr* __restrict__ hp, const double* __restrict__ mulp,
-    const double* __restrict__ prp, int pp, const double* __restrict__ xrow, int64_t xslot) {
+    smx_part* __restrict__ parts, double* __restrict__ mul, double* __restrict__ pr,
+    double* __restrict__ fr, const double* __restrict__ recv, int nranks,
+    int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,
+    const double* __restrict__ xrow, int64_t xslot) {
+    BlkHdr* __restrict__ hs = h;   // the chain state (cfs) lives in the block's header
     constexpr int D = L - 1;
     constexpr int NT = kBlkNT;
-    // scan rounds: the pipelined form evaluates one column per thread at a time (its chains carry
-    // twice the operands and it must stay within 72 VGPRs); the others issue all four at once
-    constexpr int SCANU = LAG ? 1 : 4;
-    constexpr int NQ = 2 * kBlkMax + 1;
+    constexpr int SCANU = 4;   // scan rounds: all four columns of a thread issued at once
     __shared__ BlkPiv s_pv;
     __shared__ double s_col[3][kBlkMax];      // pr_q at columns c, m, cf
-    // LAG: the chain's pivots (previous block's, then this block's), row r's multipliers, the
-    // pr_q values at columns c, m, cf, and one operand row per thread
-    __shared__ BlkPiv2 s_all;
-    __shared__ double s_mrall[NQ];
-    __shared__ double s_colall[3][NQ];
-    __shared__ double s_op[LAG ? NT : 1][NQ];
     __shared__ int s_tmp[NT / kWave];
     __shared__ Decision s_d;
     __shared__ int s_nb, s_c;
     __shared__ int64_t s_off;
     __shared__ double s_e, s_fc, s_pm, s_pa;
-    // PP > 0: the previous block's pivots (with y), its pivot rows at columns c, m, cf, and
-    // whether every one of its pivot elements is inside the fast-division window
-    constexpr int PPS = PP > 0 ? PP : 1;
-    __shared__ BlkPiv s_pvp;
-    __shared__ double s_colp[3][PPS];
-    __shared__ int s_okp;
-    static_assert(PP == 0 || (!SH && !LAG && PP <= kBlkMax), "prefix: unsharded register form");
     const int tid = threadIdx.x;
     const int b = blockIdx.x, G = gridDim.x;
     SMX_BLK_STAMP(0);
-    if (!LAG) pp = 0;
     // The stop flag is loaded together with the decision's operands and tested after them (one
     // memory round trip instead of two): on a stopped chain those loads read stale scratch and
     // their results are discarded.
     const int stopped = ctl->term;
     const int sp = (parity + D) & 1;   // step parity of block step D
     const int C = m + 1;
-    if constexpr (LAG) {
-        if (tid < pp) {   // (pp, D <= kBlkMax: lanes of the first wave)
-            const int q = tid;
-            s_all.r[q] = hp->r[q];
-            s_all.c[q] = hp->c[q];
-            s_all.e[q] = hp->e[q];
-        }
-        if (tid < D) {
-            s_all.r[pp + tid] = h->r[tid];
-            s_all.c[pp + tid] = h->c[tid];
-            s_all.e[pp + tid] = h->e[tid];
-        }
-    } else {
-        blk_load_pivots(h, D, &s_pv);
-    }
+    blk_load_pivots(h, D, &s_pv);
     if (SH) {
         if (tid == 0) {
             // full exchange: recv = the gathered send slots; light (xslot = SMX_SHARD_HDR): recv
@@ -852,20 +779,6 @@ __device__ __forceinline__ bool blk_step_body(
             s_off = sd.off;
         }
     } else if (tid < kWave) {
-        if constexpr (PP > 0) {   // (issued with the records' loads: the same round trip)
-            bool okp = true;
-            if (tid < PP) {
-                const double e = hp->e[tid];
-                const FastDiv fd = fd_prep(e);
-                s_pvp.r[tid] = hp->r[tid];
-                s_pvp.c[tid] = hp->c[tid];
-                s_pvp.e[tid] = e;
-                s_pvp.y[tid] = fd.y;
-                okp = fd.ok;
-            }
-            okp = __all(okp);
-            if (tid == 0) s_okp = okp ? 1 : 0;
-        }
         // the decision of step D from its records (every workgroup, identically)
         const int c = hs->cfs[blk_slot(D, P, bn)];
         int nb;
@@ -928,11 +841,7 @@ __device__ __forceinline__ bool blk_step_body(
     const int r_local = (r >= row0 && r < row0 + rows) ? r - row0 : -1;
     const double* prow = SH ? (xrow ? xrow : recv + s_off) : nullptr;   // T_{k+D}[r][*] (sharded)
     double mqr[kBlkMax];
-    if constexpr (LAG) {
-        if (tid < pp) s_mrall[tid] = mulp[(int64_t)r_local * kBlkMax + tid];
-        if (tid < D) s_mrall[pp + tid] = mul[(int64_t)r_local * kBlkMax + tid];
-        __syncthreads();
-    } else if (!SH) {
+    if (!SH) {
 #pragma unroll
         for (int q = 0; q < D; ++q) mqr[q] = mul[(int64_t)r_local * kBlkMax + q];
 #pragma unroll
@@ -943,37 +852,10 @@ __device__ __forceinline__ bool blk_step_body(
     const BlkPiv pvD = blk_pv_regs<D>(s_pv, &okD);
     auto prv = [&](int j) -> double {
         if (SH) return prow[j];
-        if constexpr (LAG) {
-            double* op = s_op[LAG ? tid : 0];
-#pragma unroll
-            for (int q = 0; q < kBlkMax; ++q)
-                if (q < pp) op[q] = prp[(int64_t)q * ld + j];
-#pragma unroll
-            for (int q = 0; q < D; ++q) op[pp + q] = pr[(int64_t)q * ld + j];
-            return blk_chain_rolled(T[(int64_t)r_local * ld + j], r_local, j, s_all, pp + D, op,
-                                    s_mrall);
-        }
         double x = T[(int64_t)r_local * ld + j];
         double p[kBlkMax];
-        if constexpr (PP > 0) {   // both chains' operands in one round trip
-            double pP[PPS], mP[PPS];
-#pragma unroll
-            for (int q = 0; q < PP; ++q) {
-                pP[q] = prp[(int64_t)q * ld + j];
-                mP[q] = mulp[(int64_t)r_local * kBlkMax + q];
-            }
-            blk_load_col<D>(pr, ld, j, p);
-#pragma unroll
-            for (int q = 0; q < PP; ++q) {
-                blk_pin(pP[q]);
-                blk_pin(mP[q]);
-            }
-            blk_pin(x);
-            x = blk_pfx<PP>(x, r_local, j, s_pvp, s_okp != 0, pP, mP);
-        } else {
-            blk_load_col<D>(pr, ld, j, p);
-            blk_pin(x);
-        }
+        blk_load_col<D>(pr, ld, j, p);
+        blk_pin(x);
         uint32_t wt = 0;
         const double v = blk_chain_fd<D>(x, r_local, j, pvD, p, mqr, wt);
         if (okD && __all(wt < kWinSpan)) return v;
@@ -995,7 +877,7 @@ __device__ __forceinline__ bool blk_step_body(
     // the benchmark's LPs lies within the first ~60 columns; the earlier first round of 1024
     // columns cost 7 chains and 7 (D + 2) loads per thread on every step: tools/trace_planner.hip,
     // profiles/r03b/).  Same chains on the same operands: the same values.
-    if (!SH && !LAG && nb == SMX_NONE) {
+    if (!SH && nb == SMX_NONE) {
         c = d.c;
         const double* Tr = T + (int64_t)r_local * ld;
         const int S = ((C + G - 1) / G + 1) & ~1;
@@ -1008,45 +890,10 @@ __device__ __forceinline__ bool blk_step_body(
 #pragma unroll
         for (int k = 0; k < NSC; ++k) jj[2 + k] = tid + k * NT;
         double x[NJ], pq[NJ][kBlkMax], fv[NJ];
-        double xr[NJ];
-        if constexpr (PP > 0) {
-            // row r of X_{b+1} at the NJ columns first (one round trip of its own: holding both
-            // chains' operands at once would double the registers of the fused phase)
-            double pP[NJ][PPS], mP[PPS];
-#pragma unroll
-            for (int u = 0; u < NJ; ++u) {
-                const int jc = min(jj[u], C - 1);
-                xr[u] = Tr[jc];
-#pragma unroll
-                for (int q = 0; q < PP; ++q) pP[u][q] = prp[(int64_t)q * ld + jc];
-            }
-#pragma unroll
-            for (int q = 0; q < PP; ++q) mP[q] = mulp[(int64_t)r_local * kBlkMax + q];
-#pragma unroll
-            for (int u = 0; u < NJ; ++u) {
-                blk_pin(xr[u]);
-#pragma unroll
-                for (int q = 0; q < PP; ++q) blk_pin(pP[u][q]);
-            }
-#pragma unroll
-            for (int q = 0; q < PP; ++q) blk_pin(mP[q]);
-            uint32_t wtp = 0;
-            double yr[NJ];
-#pragma unroll
-            for (int u = 0; u < NJ; ++u)
-                yr[u] = blk_chain_fd<PPS>(xr[u], r_local, jj[u], s_pvp, pP[u], mP, wtp);
-            if (!s_okp || !__all(wtp < kWinSpan)) {
-#pragma unroll
-                for (int u = 0; u < NJ; ++u)
-                    yr[u] = blk_chain<PPS>(xr[u], r_local, jj[u], s_pvp, pP[u], mP);
-            }
-#pragma unroll
-            for (int u = 0; u < NJ; ++u) xr[u] = yr[u];
-        }
 #pragma unroll
         for (int u = 0; u < NJ; ++u) {
             const int jc = min(jj[u], C - 1);
-            x[u] = PP > 0 ? xr[u] : Tr[jc];
+            x[u] = Tr[jc];
             fv[u] = fo[jc];
 #pragma unroll
             for (int q = 0; q < D; ++q) pq[u][q] = pr[(int64_t)q * ld + jc];
@@ -1225,27 +1072,7 @@ __device__ __forceinline__ bool blk_step_body(
     }
     // step L's pivots in LDS-broadcast form: s_pv[D] = this pivot; the pivot rows at the columns
     // the row pass reads (uniform)
-    if constexpr (LAG) {
-        const int n = pp + D;
-        if (tid == 0) {
-            s_all.r[n] = r_local;
-            s_all.c[n] = c;
-            s_all.e[n] = e;
-            s_colall[1][n] = s_pm;
-            s_colall[2][n] = s_pa;
-        }
-        if (tid < pp) {
-            const int q = tid;
-            s_colall[0][q] = prp[(int64_t)q * ld + c];
-            s_colall[1][q] = prp[(int64_t)q * ld + m];
-            if (cf != SMX_NONE) s_colall[2][q] = prp[(int64_t)q * ld + cf];
-        }
-        if (tid < D) {
-            s_colall[0][pp + tid] = pr[(int64_t)tid * ld + c];
-            s_colall[1][pp + tid] = pr[(int64_t)tid * ld + m];
-            if (cf != SMX_NONE) s_colall[2][pp + tid] = pr[(int64_t)tid * ld + cf];
-        }
-    } else {
+    {
         __syncthreads();   // s_pa / s_pm / s_col of the phase-2 path are written before this
         if (tid == 0) {
             s_pv.r[D] = r_local;
@@ -1258,12 +1085,6 @@ __device__ __forceinline__ bool blk_step_body(
             s_col[0][tid] = pr[(int64_t)tid * ld + c];
             s_col[1][tid] = pr[(int64_t)tid * ld + m];
             if (cf != SMX_NONE) s_col[2][tid] = pr[(int64_t)tid * ld + cf];
-        }
-        if (PP > 0 && tid >= kWave && tid < kWave + PP) {   // (a wave the stores above spare)
-            const int q = tid - kWave;
-            s_colp[0][q] = prp[(int64_t)q * ld + c];
-            s_colp[1][q] = prp[(int64_t)q * ld + m];
-            if (cf != SMX_NONE) s_colp[2][q] = prp[(int64_t)q * ld + cf];
         }
     }
     __syncthreads();
@@ -1282,26 +1103,22 @@ __device__ __forceinline__ bool blk_step_body(
     BlkPiv pvL;
     bool okL = true;
     double colv[3][kBlkMax];
-    if constexpr (!LAG) {
-        pvL = blk_pv_regs<L>(s_pv, &okL);
+    pvL = blk_pv_regs<L>(s_pv, &okL);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 3; ++k) {
 #pragma unroll
-            for (int q = 0; q < L; ++q) colv[k][q] = s_col[k][q];
+        for (int q = 0; q < L; ++q) colv[k][q] = s_col[k][q];
 #pragma unroll
-            for (int q = 0; q < L; ++q) blk_pin(colv[k][q]);
-        }
+        for (int q = 0; q < L; ++q) blk_pin(colv[k][q]);
     }
     // Chain-result cache (the register form): step L keeps T_{k+L}[i][m] and T_{k+L}[i][cf] --
     // the values its records were built on -- in cb / ca by step parity, so step L+1 takes its
     // multipliers T_{k+L}[i][c] (c = this cf in phase 2) as they are and its "-b" values with ONE
     // more step, instead of re-deriving both by chains of length L from T_k; only the new
     // column's chain remains (L+1 chain steps per row instead of 3L-1).  Same operations on the
-    // same operands in the same order as the full chains, so the same bits.  The pipelined (LAG)
-    // form keeps the raw T_k columns (colm, colc) instead.
-    double* colm = fr + 2 * ld;
-    double* colc = colm + rows;
-    double* cca = colc + 2 * (int64_t)rows;
+    // same operands in the same order as the full chains, so the same bits.  (The layout's first
+    // 3 R doubles after the f-rows are unused since the pipelined planner left.)
+    double* cca = fr + 2 * ld + 3 * (int64_t)rows;
     double* ccb = cca + 2 * (int64_t)rows;
     const bool reuse_c = D > 0 && c == s_c;   // phase 2: c is the column of step D's records
     double* mT = blk_mulT(mul, rows + 1);
@@ -1309,73 +1126,19 @@ __device__ __forceinline__ bool blk_step_body(
     for (int i = b * NT + tid; i < rows; i += G * NT) {
         const double* row = T + (int64_t)i * ld;
         double* mr = mul + (int64_t)i * kBlkMax;
-        const double xc = reuse_c ? (LAG ? colc : cca)[(int64_t)(D & 1) * rows + i] : row[c];
-        const double xb = D > 0 ? (LAG ? colm[i] : ccb[(int64_t)(D & 1) * rows + i]) : row[m];
+        const double xc = reuse_c ? cca[(int64_t)(D & 1) * rows + i] : row[c];
+        const double xb = D > 0 ? ccb[(int64_t)(D & 1) * rows + i] : row[m];
         const double xa = cf != SMX_NONE ? row[cf] : 0.0;
-        if (LAG && D == 0) colm[i] = xb;
-        if (LAG && cf != SMX_NONE) colc[(int64_t)(L & 1) * rows + i] = xa;
         double bv, a;
-        if constexpr (LAG) {
-            // row i's multipliers (previous block's, then this block's) in its LDS operand row
-            double* op = s_op[LAG ? tid : 0];
-            const double* mrp = mulp + (int64_t)i * kBlkMax;
-#pragma unroll
-            for (int q = 0; q < kBlkMax; ++q)
-                if (q < pp) op[q] = mrp[q];
-#pragma unroll
-            for (int q = 0; q < D; ++q) op[pp + q] = mr[q];
-            const int n = pp + D;
-            const double mc = blk_chain_rolled(xc, i, c, s_all, n, s_colall[0], op);
-            mr[D] = mc;                                              // T_{k+D}[i][c]
-            // (and transposed: the next block's planner may be the prefix form, whose row pass
-            // reads this block's multipliers from blk_mulT)
-            blk_mulT(mul, rows + 1)[(int64_t)D * (rows + 1) + i] = mc;
-            op[n] = mc;
-            if (L == P) {   // the sweep's per-row flag (this block's multipliers, blk_rflags)
-                bool bnd = bnd_or_zero(mc), zero = (dbits(mc) << 1) == 0;
-                bool piv = i == s_all.r[n];
-                for (int q = 0; q < D; ++q) {
-                    bnd = bnd && bnd_or_zero(op[pp + q]);
-                    zero = zero || (dbits(op[pp + q]) << 1) == 0;
-                    piv = piv || i == s_all.r[pp + q];
-                }
-                blk_rflags(mul, rows + 1)[i] = blk_rflag(piv, bnd, zero);
-            }
-            bv = blk_chain_rolled(xb, i, m, s_all, n + 1, s_colall[1], op);
-            a = cf != SMX_NONE ? blk_chain_rolled(xa, i, cf, s_all, n + 1, s_colall[2], op) : 0.0;
-        } else {
+        {
             double mq[kBlkMax];
             double x3[3] = {xc, xb, xa};
-            double mP[PPS];
 #pragma unroll
             for (int q = 0; q < D; ++q) mq[q] = mT[(int64_t)q * (rows + 1) + i];
-            if constexpr (PP > 0) {
-                const double* mTp = blk_mulT(mulp, rows + 1);
-#pragma unroll
-                for (int q = 0; q < PP; ++q) mP[q] = mTp[(int64_t)q * (rows + 1) + i];
-            }
 #pragma unroll
             for (int q = 0; q < D; ++q) blk_pin(mq[q]);
 #pragma unroll
             for (int k = 0; k < 3; ++k) blk_pin(x3[k]);
-            if constexpr (PP > 0) {
-                // the values read from X_b (not the caches) through the previous block's pivots
-#pragma unroll
-                for (int q = 0; q < PP; ++q) blk_pin(mP[q]);
-                const bool pc = !reuse_c, pb = D == 0, pa = cf != SMX_NONE;
-                uint32_t wtp = 0;
-                double y3[3] = {x3[0], x3[1], x3[2]};
-                if (pc) y3[0] = blk_chain_fd<PPS>(x3[0], i, c, s_pvp, s_colp[0], mP, wtp);
-                if (pb) y3[1] = blk_chain_fd<PPS>(x3[1], i, m, s_pvp, s_colp[1], mP, wtp);
-                if (pa) y3[2] = blk_chain_fd<PPS>(x3[2], i, cf, s_pvp, s_colp[2], mP, wtp);
-                if (!s_okp || !__all(wtp < kWinSpan)) {
-                    if (pc) y3[0] = blk_chain<PPS>(x3[0], i, c, s_pvp, s_colp[0], mP);
-                    if (pb) y3[1] = blk_chain<PPS>(x3[1], i, m, s_pvp, s_colp[1], mP);
-                    if (pa) y3[2] = blk_chain<PPS>(x3[2], i, cf, s_pvp, s_colp[2], mP);
-                }
-#pragma unroll
-                for (int k = 0; k < 3; ++k) x3[k] = y3[k];
-            }
             // x3[0]: T_{k+D}[i][c] itself when cached (reuse_c), else T_k[i][c]; x3[1]:
             // T_{k+D}[i][m] (cached) from step 1 on, T_k[i][m] at step 0
             constexpr int QB = D > 0 ? D : 0;
@@ -1419,31 +1182,18 @@ __device__ __forceinline__ bool blk_step_body(
 #define SMX_BLK_STEP_PARAMS                                                                         \
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int row0,      \
         int P, int parity, int bn, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,              \
-        BlkHdr* __restrict__ hs, smx_part* __restrict__ parts, double* __restrict__ mul,           \
-        double* __restrict__ pr, double* __restrict__ fr, const double* __restrict__ recv,         \
-        int nranks, int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,        \
-        const BlkHdr* __restrict__ hp, const double* __restrict__ mulp,                            \
-        const double* __restrict__ prp, int pp, const double* __restrict__ xrow, int64_t xslot
+        smx_part* __restrict__ parts, double* __restrict__ mul, double* __restrict__ pr,           \
+        double* __restrict__ fr, const double* __restrict__ recv, int nranks,                      \
+        int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap,                    \
+        const double* __restrict__ xrow, int64_t xslot
 #define SMX_BLK_STEP_ARGS                                                                           \
-    T, ld, rows, m, flen, fscan, row0, P, parity, bn, ctl, h, hs, parts, mul, pr, fr, recv, nranks, \
-        log, xhist, log_cap, hp, mulp, prp, pp, xrow, xslot
+    T, ld, rows, m, flen, fscan, row0, P, parity, bn, ctl, h, parts, mul, pr, fr, recv, nranks,     \
+        log, xhist, log_cap, xrow, xslot
 
-// The planner launches.  The pipelined form runs beside a sweep (5 waves per SIMD of 88 VGPRs at
-// P = 8), so it must fit in the 72 VGPRs per SIMD lane the sweep leaves: its rolled LDS-operand
-// chains hold it at 34-41 (the unrolled register form of k_blk_step: 36-117).
+// The register-form planner launch (row-sharded chains; unsharded with smx_tune_block_planner(1))
 template <int L, bool SH>
 __global__ __launch_bounds__(kBlkNT) void k_blk_step(SMX_BLK_STEP_PARAMS) {
-    blk_step_body<L, SH, false>(SMX_BLK_STEP_ARGS);
-}
-template <int L>
-__global__ __launch_bounds__(kBlkNT) void k_blk_step_lag(SMX_BLK_STEP_PARAMS) {
-    blk_step_body<L, false, true>(SMX_BLK_STEP_ARGS);
-}
-// Pipelined register form: the register form on X_b with every read prefixed by the previous
-// block's PP pivots (blk_pfx); for the planner's own CUs of a partitioned chain
-template <int L, int PP>
-__global__ __launch_bounds__(kBlkNT) void k_blk_step_pfx(SMX_BLK_STEP_PARAMS) {
-    blk_step_body<L, false, false, PP>(SMX_BLK_STEP_ARGS);
+    blk_step_body<L, SH>(SMX_BLK_STEP_ARGS);
 }
 
 #undef SMX_BLK_STEP_PARAMS
@@ -1963,26 +1713,6 @@ __global__ __launch_bounds__(kWave) void k_blk_publish(const BlkHdr* __restrict_
                                                        int nparts, int slot, int parity,
                                                        smx_ctl* __restrict__ ctl) {
     blk_publish_wave(h, parts, nparts, slot, parity, ctl);
-}
-
-// End of a pipelined chain: the table after the d pivots it applied belongs in
-// buf[(parity + d) & 1] (the ping-pong convention of every chain); the chain's out-of-place sweeps
-// put it there unless a terminal outcome cut the chain short, and then this copies it over
-// (every workgroup returns at once otherwise).
-__global__ __launch_bounds__(kUpdBlock) void k_blk_settle(double* buf0, double* buf1,
-                                                          int64_t ndbl, int parity,
-                                                          const smx_ctl* __restrict__ ctl,
-                                                          const BlkHdr* __restrict__ hs) {
-    const int64_t d = ctl->npivots - hs->np0;
-    const int target = (parity + (int)(d & 1)) & 1;
-    const int loc = hs->loc;
-    if (loc == target) return;
-    const dbl2* src = reinterpret_cast<const dbl2*>(loc ? buf1 : buf0);
-    dbl2* dst = reinterpret_cast<dbl2*>(target ? buf1 : buf0);
-    const int64_t n2 = ndbl / 2;
-    for (int64_t k = (int64_t)blockIdx.x * kUpdBlock + threadIdx.x; k < n2;
-         k += (int64_t)gridDim.x * kUpdBlock)
-        dst[k] = src[k];
 }
 
 }  // namespace

@@ -52,7 +52,7 @@ static_assert(sizeof(smx_part) == 32, "smx_part layout");
 #include "smx_batch.hpp"
 #include "smx_resident.hpp"
 #include "smx_block.hpp"
-#include "smx_plan.hpp"
+#include "smx_window.hpp"
 #include "smx_host.hpp"
 #include "smx_intfirst.hpp"
 
@@ -185,7 +185,6 @@ int variant_for(const smx_shape& s) {
 // is resident at once and the balanced unit ranges finish together (no second residency round).
 // The host-side caches below are shared by smx_mshard_run's per-device threads: one mutex.
 std::mutex g_cache_mu;
-std::mutex g_pipe_mu;   // the pipelined chains' per-device streams (blk_pipe_for)
 
 // Resident 256-thread blocks per CU of `fn` by the occupancy API (registers and LDS), one block
 // of margin below its answer, cached; at most `cap`.
@@ -220,11 +219,8 @@ int resident_bpc(const void* fn, int cap) {
     return bpc < cap ? bpc : cap;
 }
 
-// CUs the launches of this thread may fill: the device's, or fewer while a pipelined chain runs
-// its sweeps on a CU-masked stream (CusScope)
-thread_local int t_cus = 0;
+// CUs of the current device
 int num_cus() {
-    if (t_cus > 0) return t_cus;
     static int cus[64] = {0};
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -497,9 +493,9 @@ int block_size(int k, int P, int b) {
 using BlkSweepFn = void (*)(double*, double*, int64_t, int, int, const BlkHdr*, const double*,
                            const double*, BlkHdr*, int, int);
 using BlkStepFn = void (*)(const double*, int64_t, int, int, int, int, int, int, int, int,
-                           smx_ctl*, BlkHdr*, BlkHdr*, smx_part*, double*, double*, double*,
-                           const double*, int, int32_t*, double*, int64_t, const BlkHdr*,
-                           const double*, const double*, int, const double*, int64_t);
+                           smx_ctl*, BlkHdr*, smx_part*, double*, double*, double*,
+                           const double*, int, int32_t*, double*, int64_t, const double*,
+                           int64_t);
 using BshPackFn = void (*)(const double*, int64_t, int, int, int, int, int, const smx_ctl*,
                            const BlkHdr*, const smx_part*, int, const double*, const double*,
                            double*);
@@ -520,37 +516,9 @@ BlkStepFn blk_step_pick(int L, std::integer_sequence<int, Is...>) {
     static const BlkStepFn t[] = {k_blk_step<Is + 1, SH>...};
     return t[L - 1];
 }
-template <int... Is>
-BlkStepFn blk_lag_pick(int L, std::integer_sequence<int, Is...>) {
-    static const BlkStepFn t[] = {k_blk_step_lag<Is + 1>...};
-    return t[L - 1];
-}
-
-template <bool SH, bool LAG>
+template <bool SH>
 BlkStepFn blk_step_fn_sh(int L) {
-    using All = std::make_integer_sequence<int, kBlkMax>;
-    if (LAG) return blk_lag_pick(L, All{});
-    return blk_step_pick<SH>(L, All{});
-}
-
-using BlkPlanFn = void (*)(const double*, int64_t, int, int, int, int, int, int, smx_ctl*,
-                          BlkHdr*, smx_part*, double*, double*, double*, int32_t*, double*,
-                          int64_t, uint64_t*);
-template <int... Is>
-BlkPlanFn blk_plan_pick(int P, std::integer_sequence<int, Is...>) {
-    static const BlkPlanFn t[] = {k_blk_plan<Is + 1>...};
-    return t[P - 1];
-}
-
-// smx_tune_block_persist: 1 plans every block of an unsharded, unpipelined chain in ONE
-// persistent launch (k_blk_plan, smx_plan.hpp) where each thread owns at most one row; 0 one
-// launch per pivot (k_blk_step).
-int g_block_persist = 0;
-bool plan_persistent(const smx_shape& s) {
-    if (!g_block_persist) return false;
-    const int G = blk_parts_of(s.nparts, s.rows);
-    return s.row0 == 0 && s.rows == s.n && (int64_t)s.rows <= (int64_t)G * kBlkNT &&
-           G <= num_cus();
+    return blk_step_pick<SH>(L, std::make_integer_sequence<int, kBlkMax>{});
 }
 
 template <int... Is>
@@ -565,15 +533,20 @@ struct BlkPtrs {
     BlkLayout L;
     BlkHdr* h[2];
     smx_part* parts;
-    double *mul[2], *pr[2], *fr;
+    double *mul[2], *pr[2], *fr, *win;
 };
-// Planner workgroups of a launch: blk_parts_of, or fewer in a pipelined chain whose planner runs
-// on a few CUs of its own (t_parts_cap; every launch of one chain uses the same count, since a
-// step merges the records of the step before it by that count)
-thread_local int t_parts_cap = 0;
+// smx_tune_block_planner: 0 (default) the window planner (k_blk_wstep, smx_window.hpp) on
+// unsharded chains, 1 the register-form chains (k_blk_step<L, false>); row-sharded chains always
+// run the register form (k_blk_step<L, true>).  g_block_nwin: window slots (2..kWin; tests shrink
+// it to drive the window's fallbacks).
+int g_block_planner = 0;
+int g_block_nwin = kWin;
+bool use_window(const smx_shape& s) { return g_block_planner == 0 && s.row0 == 0 && s.rows == s.n; }
+
+// Planner workgroups of a chain (every launch of one chain uses the same count, since a step
+// merges the records of the step before it by that count)
 int blk_G(const smx_shape& s) {
-    const int g = blk_parts_of(s.nparts, s.rows);
-    return t_parts_cap > 0 && t_parts_cap < g ? t_parts_cap : g;
+    return use_window(s) ? win_groups(s.rows) : blk_parts_of(s.nparts, s.rows);
 }
 
 BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
@@ -586,56 +559,48 @@ BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
     }
     b.parts = reinterpret_cast<smx_part*>(blk + b.L.parts);
     b.fr = reinterpret_cast<double*>(blk + b.L.fr);
+    b.win = reinterpret_cast<double*>(blk + b.L.win);
     return b;
 }
 
 // loc: buffer index (0/1) of T
 int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, smx_ctl* ctl,
                      const BlkPtrs& b, hipStream_t st) {
+    double* win = use_window(s) ? b.win : nullptr;
     hipLaunchKernelGGL(k_blk_start, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
                        fscan_of(s), parity, loc, s.row0, (const smx_ctl*)ctl, b.h[0], b.h[1],
-                       b.fr, b.parts);
+                       b.fr, b.parts, win, g_block_nwin);
     return (int)hipGetLastError();
 }
 
-// smx_tune_block_pipe: 1 plans block b+1 on a second stream while block b is swept (the
-// register prefix form k_blk_step_pfx where it is instantiated -- blocks of 12 or 20 after blocks
-// of 12 or 20 -- else the LDS-rolled k_blk_step_lag); 2 the same with k_blk_step_lag always;
-// 0 (default) plans every block on the solver stream right before its sweep.
-int g_block_pipe = 0;
-
-template <int PP, int... Is>
-BlkStepFn blk_pfx_pick(int L, std::integer_sequence<int, Is...>) {
-    static const BlkStepFn t[] = {k_blk_step_pfx<Is + 1, PP>...};
-    return t[L - 1];
-}
-// the register prefix form of step L after a block of pp pivots, or nullptr
-BlkStepFn blk_pfx_fn(int L, int pp) {
-    if (pp == 20 && L >= 1 && L <= 20)
-        return blk_pfx_pick<20>(L, std::make_integer_sequence<int, 20>{});
-    if (pp == 12 && L >= 1 && L <= 12)
-        return blk_pfx_pick<12>(L, std::make_integer_sequence<int, 12>{});
-    return nullptr;
-}
-
-// One planner launch of block bn (plan slot `slot`).  pp > 0 (pipelined chains): T is the
-// previous block's input table and that block's pp pivots (plan slot slot ^ 1) prefix every chain.
+// One planner launch of block bn (the register-form planner k_blk_step<L, SH>).
 int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, int parity,
                     int bn, smx_ctl* ctl, const BlkPtrs& b, const double* recv, int nranks,
-                    int32_t* log, double* xhist, int64_t log_cap, hipStream_t st, int slot = 0,
-                    int pp = 0, const double* xrow = nullptr, int64_t xslot = 0) {
-    BlkStepFn fn = sh ? blk_step_fn_sh<true, false>(L)
-                      : (pp > 0 ? blk_step_fn_sh<false, true>(L) : blk_step_fn_sh<false, false>(L));
-    if (!sh && pp > 0 && g_block_pipe == 1) {
-        const BlkStepFn f = blk_pfx_fn(L, pp);
-        if (f) fn = f;
-    }
-    const int o = slot ^ 1;
+                    int32_t* log, double* xhist, int64_t log_cap, hipStream_t st,
+                    const double* xrow = nullptr, int64_t xslot = 0) {
+    BlkStepFn fn = sh ? blk_step_fn_sh<true>(L) : blk_step_fn_sh<false>(L);
     hipLaunchKernelGGL(fn, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
-                       fscan_of(s), s.row0, P, parity, bn, ctl, b.h[slot], b.h[0], b.parts,
-                       b.mul[slot], b.pr[slot], b.fr, recv, nranks, log, xhist, log_cap,
-                       (const BlkHdr*)b.h[o], (const double*)b.mul[o], (const double*)b.pr[o],
-                       pp, xrow, xslot);
+                       fscan_of(s), s.row0, P, parity, bn, ctl, b.h[0], b.parts, b.mul[0],
+                       b.pr[0], b.fr, recv, nranks, log, xhist, log_cap, xrow, xslot);
+    return (int)hipGetLastError();
+}
+
+// One window-planner launch (block bn, step L) and, after a block's last step, the pivot rows
+int launch_blk_wstep(int L, const double* T, const smx_shape& s, int P, int parity, int bn,
+                     smx_ctl* ctl, const BlkPtrs& b, int32_t* log, double* xhist, int64_t log_cap,
+                     hipStream_t st) {
+    hipLaunchKernelGGL(k_blk_wstep, dim3(win_groups(s.rows)), dim3(kBlkNT), 0, st, T, s.ld,
+                       s.rows, s.m, s.flen, fscan_of(s), P, L, parity, bn, g_block_nwin,
+                       win_rpw(s.rows), ctl, b.h[0], b.parts, b.mul[0], b.win, log, xhist,
+                       log_cap);
+    return (int)hipGetLastError();
+}
+int launch_blk_prows(const double* T, const smx_shape& s, int P, const BlkPtrs& b,
+                     hipStream_t st) {
+    const int64_t work = std::max<int64_t>(s.m + 1, s.rows + 1);
+    const int grid = (int)std::min<int64_t>((work + kUpdBlock - 1) / kUpdBlock, num_cus() * 4);
+    hipLaunchKernelGGL(k_blk_prows, dim3(grid), dim3(kUpdBlock), 0, st, T, s.ld, s.rows, s.m, P,
+                       (const BlkHdr*)b.h[0], b.mul[0], b.pr[0]);
     return (int)hipGetLastError();
 }
 
@@ -661,18 +626,6 @@ int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
     hipLaunchKernelGGL(bsh_pack_fn(D), dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
                        s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h[0], (const smx_part*)b.parts,
                        blk_parts_of(s.nparts, s.rows), (const double*)b.mul[0], (const double*)b.pr[0], send);
-    return (int)hipGetLastError();
-}
-
-// Block bn's P planner steps in one persistent launch (plan slot 0)
-int launch_blk_plan(const double* T, const smx_shape& s, int P, int parity, int bn, smx_ctl* ctl,
-                    const BlkPtrs& b, char* blk, int32_t* log, double* xhist, int64_t log_cap,
-                    hipStream_t st) {
-    const int G = blk_parts_of(s.nparts, s.rows);
-    hipLaunchKernelGGL(blk_plan_pick(P, std::make_integer_sequence<int, kBlkMax>{}), dim3(G),
-                       dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen, fscan_of(s), parity, bn,
-                       ctl, b.h[0], b.parts, b.mul[0], b.pr[0], b.fr, log, xhist, log_cap,
-                       reinterpret_cast<uint64_t*>(blk + b.L.xr));
     return (int)hipGetLastError();
 }
 
@@ -748,109 +701,6 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
 }
 
 
-// smx_tune_block_pipe_cus: r > 0 gives the planner of a pipelined chain r CUs of every XCD and
-// the sweeps the other 32 - r (two CU-masked streams, hipExtStreamCreateWithCUMask), so the
-// planner's launches neither wait for the sweep's waves to retire nor share their CUs' issue
-// slots; parts > 0 caps the planner's workgroups (every launch of such a chain) so they all fit
-// on the planner's CUs at once.  MI355X only (256 CUs, 8 XCDs of 32); eager chains only -- a
-// captured graph's kernel nodes do not keep their stream's CU mask, so a chain enqueued under
-// stream capture runs unpartitioned.
-int g_pipe_cus = 0, g_pipe_parts = 0;
-
-// CU mask of the planner (r per XCD) or of the sweeps (the rest): bits {32x + x + 8t : x < 8,
-// t < r} -- r CUs of every XCD whether the driver maps mask bit i to XCD i / 32 or to XCD i % 8
-// (tools/cumask_probe.hip)
-void pipe_cu_mask(int r, bool planner, uint32_t m[8]) {
-    for (int w = 0; w < 8; ++w) m[w] = planner ? 0u : ~0u;
-    for (int x = 0; x < 8; ++x)
-        for (int t = 0; t < r; ++t) {
-            const int i = 32 * x + x + 8 * t;
-            if (planner) m[i / 32] |= 1u << (i % 32);
-            else m[i / 32] &= ~(1u << (i % 32));
-        }
-}
-
-// The planner stream (and, partitioned, the sweep stream) and the events ordering them against
-// the solver stream, once per device and partition.
-struct BlkPipe {
-    hipStream_t q = nullptr, sw = nullptr;
-    int r = -1;   // the partition q / sw were made for (0: unmasked planner stream, no sw)
-    hipEvent_t fork = nullptr, join = nullptr, plan[2] = {nullptr, nullptr},
-               sweep[2] = {nullptr, nullptr};
-};
-
-// *part: the chain may use the partition (q and sw CU-masked; never under stream capture, which
-// keeps the streams it finds -- nothing may be synchronised or destroyed while capturing)
-int blk_pipe_for(hipStream_t st, BlkPipe** out, bool* part) {
-    static BlkPipe cache[64];
-    int dev = 0;
-    if (hipStreamGetDevice(st, &dev) != hipSuccess) (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) return (int)hipErrorInvalidDevice;
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cap);
-    const bool capturing = cap != hipStreamCaptureStatusNone;
-    const int ncu = num_cus();
-    std::lock_guard<std::mutex> lock(g_pipe_mu);
-    BlkPipe& o = cache[dev];
-    const int r = capturing && o.q ? o.r : (!capturing && ncu == 256 ? g_pipe_cus : 0);
-    *part = !capturing && r > 0;
-    if (o.q && o.r == r) {
-        *out = &o;
-        return 0;
-    }
-    int cur = 0;
-    (void)hipGetDevice(&cur);
-    hipError_t e = hipSetDevice(dev);
-    if (o.q) {   // another partition: new streams (the old ones are drained first)
-        if (e == hipSuccess) e = hipStreamSynchronize(o.q);
-        if (e == hipSuccess && o.sw) e = hipStreamSynchronize(o.sw);
-        if (e == hipSuccess) {
-            (void)hipStreamDestroy(o.q);
-            if (o.sw) (void)hipStreamDestroy(o.sw);
-            o.q = o.sw = nullptr;
-        }
-    }
-    if (e == hipSuccess && r > 0) {
-        uint32_t mq[8], ms[8];
-        pipe_cu_mask(r, true, mq);
-        pipe_cu_mask(r, false, ms);
-        e = hipExtStreamCreateWithCUMask(&o.q, 8, mq);
-        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&o.sw, 8, ms);
-    } else if (e == hipSuccess) {
-        e = hipStreamCreateWithFlags(&o.q, hipStreamNonBlocking);
-    }
-    if (e == hipSuccess && !o.fork) {
-        hipEvent_t* evs[6] = {&o.fork, &o.join, &o.plan[0], &o.plan[1], &o.sweep[0], &o.sweep[1]};
-        for (int i = 0; i < 6 && e == hipSuccess; ++i)
-            e = hipEventCreateWithFlags(evs[i], hipEventDisableTiming);
-    }
-    (void)hipSetDevice(cur);
-    if (e != hipSuccess) {
-        if (o.q) (void)hipStreamDestroy(o.q);
-        if (o.sw) (void)hipStreamDestroy(o.sw);
-        o.q = o.sw = nullptr;
-        o.r = -1;
-        *part = false;
-        return (int)e;
-    }
-    o.r = r;
-    *out = &o;
-    return 0;
-}
-
-// the CU count (num_cus) and planner workgroup cap (blk_G) of this thread's launches, for a scope
-struct LaunchScope {
-    int cus0, parts0;
-    LaunchScope(int cus, int parts) : cus0(t_cus), parts0(t_parts_cap) {
-        t_cus = cus;
-        t_parts_cap = parts;
-    }
-    ~LaunchScope() {
-        t_cus = cus0;
-        t_parts_cap = parts0;
-    }
-};
-
 // k pivots in blocks of P: prime + first records, then per block P step launches and one sweep;
 // publish.  ev (optional): 2 events per block recorded around its sweep.  With comm (row-sharded,
 // one rank per GPU): every step launch is preceded by this rank's pack and ONE ncclAllGather of
@@ -867,14 +717,6 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     int rank = 0;
     if (light && ncclCommUserRank(comm, &rank) != ncclSuccess) return (int)hipErrorInvalidValue;
     double* xrow = light ? recv + (size_t)nranks * SMX_SHARD_HDR : nullptr;
-    BlkPipe* sqp = nullptr;
-    bool part = false;
-    if (!sh && !g_block_pipe && g_pipe_cus > 0 && !plan_persistent(s)) {
-        const int e = blk_pipe_for(st, &sqp, &part);
-        if (e) return e;
-        if (!part) sqp = nullptr;
-    }
-    LaunchScope scope(0, sqp ? g_pipe_parts : 0);
     int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, parity, ctl, bp, st);
     int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
@@ -884,17 +726,7 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
         const int Pb = block_size(k, P, bn);
         double* tin = p ? buf1 : buf0;
         double* toth = p ? buf0 : buf1;
-        if (!sh && plan_persistent(s))   // the block's Pb planner steps in one launch
-            err = launch_blk_plan(tin, s, Pb, p, bn, ctl, bp, blk, log, xhist, log_cap, st);
-        // diagnostic (smx_tune_block_pipe_cus without pipelining): the planner steps on the
-        // partition's planner CUs, in turn with the sweeps (its time on those CUs alone)
-        hipStream_t pst = st;
-        if (sqp && !err) {
-            err = (int)hipEventRecord(sqp->fork, st);
-            if (!err) err = (int)hipStreamWaitEvent(sqp->q, sqp->fork, 0);
-            pst = sqp->q;
-        }
-        for (int l = 1; l <= Pb && !err && !(!sh && plan_persistent(s)); ++l) {
+        for (int l = 1; l <= Pb && !err; ++l) {
             if (sh) {
                 err = launch_bsh_pack(l - 1, tin, s, Pb, bn, ctl, bp, send, st);
                 if (!err && !light) {
@@ -911,22 +743,21 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                     if (r != ncclSuccess) err = -1000 - (int)r;
                 }
             }
-            if (!err)   // sharded: each rank writes the x-history of the label rows it owns
+            if (!err && !sh && use_window(s))
+                err = launch_blk_wstep(l, tin, s, Pb, p, bn, ctl, bp, log, xhist, log_cap, st);
+            else if (!err)   // sharded: each rank writes the x-history of the label rows it owns
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
-                                      xhist, log_cap, pst, 0, 0, xrow,
+                                      xhist, log_cap, st, xrow,
                                       light ? (int64_t)SMX_SHARD_HDR : 0);
 #ifdef SMX_BLK_TRACE_TWICE
             // diagnostic build (tools/trace_planner.hip): a step is idempotent (it reads slot D /
             // parity sp and writes slot L / parity sp^1), so running it again times it warm
             if (!err && !sh)
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
-                                      xhist, log_cap, st, 0, 0, xrow, 0);
+                                      xhist, log_cap, st, xrow, 0);
 #endif
         }
-        if (sqp && !err) {
-            err = (int)hipEventRecord(sqp->plan[0], sqp->q);
-            if (!err) err = (int)hipStreamWaitEvent(st, sqp->plan[0], 0);
-        }
+        if (!err && !sh && use_window(s)) err = launch_blk_prows(tin, s, Pb, bp, st);
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
         const bool lastb = done + Pb >= k;   // its pivot-column pass publishes the chain
         if (!err)
@@ -939,95 +770,6 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     }
     if (err) return err;
     return bn == 0 ? launch_blk_publish(s, p, bn, ctl, bp, st) : 0;   // (k = 0: no block)
-}
-
-// ---- pipelined block chains (unsharded) ------------------------------------------------------
-
-// k pivots in blocks of P with the planner off the critical path:
-//   solver stream S: prime; plan block 0 (its steps, from X_0); then per block b:
-//                    [wait plan b] sweep b: X_b -> X_{b+1}, OUT OF PLACE (the planner of block
-//                    b+1 is reading X_b meanwhile); the last block in place when that lands the
-//                    table in buf[(parity + k) & 1]; finally publish + settle
-//   planner stream Q: per block b+1: [wait sweep b-1: X_b complete, plan slot (b+1)&1 free]
-//                    its steps from X_b, every chain prefixed by block b's pivots
-// The ragged block (k not a multiple of P) comes FIRST, so the one exposed planning is the
-// shortest.  ev (optional): 2 timing events per block around its sweep on S.
-int launch_block_chain_pipe(double* buf0, double* buf1, const smx_shape& s, int parity, int k,
-                            int P, smx_ctl* ctl, char* blk, int32_t* log, double* xhist,
-                            int64_t log_cap, hipStream_t st, hipEvent_t* ev = nullptr) {
-    BlkPipe* pp = nullptr;
-    bool part = false;
-    int err = blk_pipe_for(st, &pp, &part);
-    if (err) return err;
-    // partitioned: the solver stream forks to the sweep stream (sized grids: num_cus() below is
-    // the sweep's CU count) and joins it at the end
-    const int ncu = num_cus();
-    LaunchScope scope(part ? ncu - 8 * pp->r : 0, g_pipe_parts);
-    hipStream_t S = part ? pp->sw : st;
-    const BlkPtrs bp = blk_ptrs(s, blk);
-    const int nb = (k + P - 1) / P;
-    const int P0 = k - (nb - 1) * P;
-    auto buf = [&](int idx) { return idx ? buf1 : buf0; };
-    auto hip = [&](hipError_t e) {
-        if (!err && e != hipSuccess) err = (int)e;
-    };
-    if (part) {
-        hip(hipEventRecord(pp->fork, st));
-        hip(hipStreamWaitEvent(S, pp->fork, 0));
-    }
-    if (!err) err = launch_blk_prime(buf(parity), s, parity, parity, ctl, bp, S);
-    for (int l = 1; l <= P0 && !err; ++l)
-        err = launch_blk_step(false, l, buf(parity), s, P0, parity, 0, ctl, bp, nullptr, 0, log,
-                              xhist, log_cap, S);
-    if (nb > 1) {
-        hip(hipEventRecord(pp->fork, S));
-        hip(hipStreamWaitEvent(pp->q, pp->fork, 0));
-    }
-    int db = 0;   // pivots before block b
-    for (int b = 0; b < nb && !err; ++b) {
-        const int Pb = b == 0 ? P0 : P;
-        const int in_idx = (parity + b) & 1;
-        const bool last = b == nb - 1;
-        const int x = (db - b) & 1;   // blk_out: in place iff x + (pivots applied) is even
-        if (b > 0) hip(hipStreamWaitEvent(S, pp->plan[b & 1], 0));
-        if (ev) hip(hipEventRecord(ev[2 * b], S));
-        if (!err)
-            err = launch_block_sweep(buf(in_idx), buf(in_idx ^ 1), s, Pb, blk, bp.L, S, b & 1,
-                                     last ? x : -1, in_idx, x, last ? ctl : nullptr, nb,
-                                     (parity + k) & 1);
-        if (ev) hip(hipEventRecord(ev[2 * b + 1], S));
-        if (!last) {
-            hip(hipEventRecord(pp->sweep[b & 1], S));
-            if (b >= 1) hip(hipStreamWaitEvent(pp->q, pp->sweep[(b - 1) & 1], 0));
-            const int pnext = (parity + db + Pb) & 1;   // pivot parity at block b+1's start
-            for (int l = 1; l <= P && !err; ++l)
-                err = launch_blk_step(false, l, buf(in_idx), s, P, pnext, b + 1, ctl, bp, nullptr,
-                                      0, log, xhist, log_cap, pp->q, (b + 1) & 1, Pb);
-            hip(hipEventRecord(pp->plan[(b + 1) & 1], pp->q));
-        }
-        db += Pb;
-    }
-    if (!err)
-        hipLaunchKernelGGL(k_blk_settle, dim3(num_cus() * 4), dim3(kUpdBlock), 0, S, buf0, buf1,
-                           (int64_t)(s.rows + 1) * s.ld, parity, (const smx_ctl*)ctl,
-                           (const BlkHdr*)bp.h[0]);
-    if (!err) err = (int)hipGetLastError();
-    if (part) {   // join (also after an error: the solver stream must not run ahead of S)
-        const hipError_t e1 = hipEventRecord(pp->join, S);
-        const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, pp->join, 0) : e1;
-        if (!err && e2 != hipSuccess) err = (int)e2;
-    }
-    return err;
-}
-
-// The block chain of smx_block_run: pipelined when enabled and there is more than one block.
-int launch_block_any(double* buf0, double* buf1, const smx_shape& s, int parity, int k, int P,
-                     smx_ctl* ctl, char* blk, int32_t* log, double* xhist, int64_t log_cap,
-                     hipStream_t st, hipEvent_t* ev = nullptr) {
-    if (g_block_pipe && k > P)
-        return launch_block_chain_pipe(buf0, buf1, s, parity, k, P, ctl, blk, log, xhist, log_cap,
-                                       st, ev);
-    return launch_block_chain(buf0, buf1, s, parity, k, P, ctl, blk, log, xhist, log_cap, st, ev);
 }
 
 bool block_args_ok(const smx_shape* shape, int k, int P, const void* blk, int64_t blk_bytes) {
@@ -1779,23 +1521,11 @@ int smx_tune_block_form(int32_t form) {
     return prev;
 }
 
-int smx_tune_block_persist(int32_t on) {
-    const int prev = g_block_persist;
-    if (on >= 0) g_block_persist = on ? 1 : 0;
-    return prev;
-}
-
-int smx_tune_block_pipe(int32_t on) {
-    const int prev = g_block_pipe;
-    if (on >= 0) g_block_pipe = on == 2 ? 2 : (on ? 1 : 0);
-    return prev;
-}
-
-int smx_tune_block_pipe_cus(int32_t cus_per_xcd, int32_t parts) {
-    if (cus_per_xcd > 16 || parts > kBlkPartsMax) return -1;
-    const int prev = g_pipe_cus;
-    if (cus_per_xcd >= 0) g_pipe_cus = cus_per_xcd;
-    if (parts >= 0) g_pipe_parts = parts;
+int smx_tune_block_planner(int32_t planner, int32_t nwin) {
+    const int prev = g_block_planner;
+    if (planner == 0 || planner == 1) g_block_planner = planner;
+    if (nwin >= 2 && nwin <= kWin) g_block_nwin = nwin;
+    else if (nwin == 0) g_block_nwin = kWin;
     return prev;
 }
 
@@ -1829,7 +1559,7 @@ int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t pa
     if (!block_args_ok(shape, k, pivots, blk, blk_bytes) || buf0 == buf1 || !ctl)
         return (int)hipErrorInvalidValue;
     if (k == 0) return 0;
-    return launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+    return launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
                             static_cast<char*>(blk), log, xhist, log_cap, S(stream));
 }
 
@@ -1858,7 +1588,7 @@ int smx_block_run_timed(double* buf0, double* buf1, const smx_shape* shape, int3
     hipEvent_t* ev = nullptr;
     if (timer_events((size_t)(2 * nb + 2), &ev)) return (int)hipErrorOutOfMemory;
     (void)hipEventRecord(ev[2 * nb], st);
-    int err = launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+    int err = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
                                static_cast<char*>(blk), log, xhist, log_cap, st, ev);
     (void)hipEventRecord(ev[2 * nb + 1], st);
     if (defer) {
@@ -1889,7 +1619,7 @@ int smx_block_graph_create(double* buf0, double* buf1, const smx_shape* shape, i
         delete g;
         return (int)err;
     }
-    int lerr = launch_block_any(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
+    int lerr = launch_block_chain(buf0, buf1, *shape, parity & 1, k, pivots, ctl,
                                 static_cast<char*>(blk), log, xhist, log_cap, st);
     err = hipStreamEndCapture(st, &g->graph);
     if (lerr || err != hipSuccess) {
@@ -2040,7 +1770,7 @@ int smx_bshard_step_light(const double* T, const smx_shape* shape, int32_t step,
         return (int)hipErrorInvalidValue;
     return launch_blk_step(true, step, T, *shape, pivots, parity & 1, block, ctl,
                            blk_ptrs(*shape, static_cast<char*>(blk)), hdrs, nranks, log, xhist,
-                           log_cap, S(stream), 0, 0, row, SMX_SHARD_HDR);
+                           log_cap, S(stream), row, SMX_SHARD_HDR);
 }
 
 int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_t pivots,
@@ -2241,7 +1971,7 @@ int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
             for (int q = 0; q < nranks && !err; ++q)
                 err = launch_blk_step(true, l, buf(q, p), ranks[q].shape, Pb, p, bn,
                                       ranks[q].ctl, bp[q], ranks[q].recv, nranks, ranks[q].log,
-                                      ranks[q].xhist, ranks[q].log_cap, on(q), 0, 0,
+                                      ranks[q].xhist, ranks[q].log_cap, on(q),
                                       light ? xrow(q) : nullptr,
                                       light ? (int64_t)SMX_SHARD_HDR : 0);
         }

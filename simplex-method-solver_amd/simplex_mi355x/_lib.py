@@ -112,7 +112,7 @@ EXPORTS = (
     "smx_copy_probe", "smx_shard_folds_pack", "smx_tune_fold",
     "smx_tune_resident", "smx_tune_resident_overlap", "smx_tune_resident_timeout", "smx_resident_trace", "smx_resident_bytes",
     "smx_resident_run", "smx_fastdiv_check", "smx_fastdiv_check_bounded",
-    "smx_tune_block", "smx_tune_block_pipe", "smx_tune_block_pipe_cus", "smx_tune_block_form", "smx_tune_block_persist", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
+    "smx_tune_block", "smx_tune_block_form", "smx_tune_block_planner", "smx_block_bytes", "smx_block_run", "smx_block_run_timed",
     "smx_block_timed_read",
     "smx_block_graph_create",
     "smx_bshard_bytes", "smx_bshard_run", "smx_bshard_run_timed", "smx_bshard_graph_create",
@@ -201,10 +201,8 @@ def load():
         "smx_mshard_graph_create": ([ctypes.POINTER(Rank), i32, i32, i32, i32,
                                      ctypes.POINTER(vp)], ctypes.c_int),
         "smx_tune_block": ([i32], ctypes.c_int),
-        "smx_tune_block_pipe": ([i32], ctypes.c_int),
-        "smx_tune_block_pipe_cus": ([i32, i32], ctypes.c_int),
         "smx_tune_block_form": ([i32], ctypes.c_int),
-        "smx_tune_block_persist": ([i32], ctypes.c_int),
+        "smx_tune_block_planner": ([i32, i32], ctypes.c_int),
         "smx_block_bytes": ([sp, ctypes.POINTER(i32)], ctypes.c_int64),
         "smx_block_run": ([vp, vp, sp, i32, i32, i32, vp, vp, i64, vp, vp, i64, vp],
                           ctypes.c_int),
@@ -298,37 +296,21 @@ def block_plan(shape, pivots: int = 0) -> tuple[int, int] | None:
 
 
 def tune_block(pivots: int = -1) -> int:
-    """smx_tune_block: 0 automatic, 1 never, 2..16 pivots per sweep, -1 query only; returns the
+    """smx_tune_block: 0 automatic, 1 never, 2..24 pivots per sweep, -1 query only; returns the
     previous setting."""
     return int(load().smx_tune_block(pivots))
 
 
-def tune_block_persist(on: int = -1) -> int:
-    """smx_tune_block_persist: 1 plans each block of an unsharded chain in one persistent launch
-    (k_blk_plan), 0 one launch per pivot (k_blk_step); -1 only queries.  Returns the previous."""
-    return int(load().smx_tune_block_persist(on))
+def tune_block_planner(planner: int = -1, nwin: int = -1) -> int:
+    """smx_tune_block_planner: 0 the window planner (the default), 1 the register-form chains, -1
+    query only; ``nwin`` window slots 2..64 (0: 64, -1: keep).  Returns the previous planner."""
+    return int(load().smx_tune_block_planner(planner, nwin))
 
 
 def tune_block_form(form: int = -1) -> int:
     """smx_tune_block_form: 0 automatic, 4 pivot-row slices in registers, 5 in LDS; any other
     value only queries; returns the previous setting."""
     return int(load().smx_tune_block_form(form))
-
-
-def tune_block_pipe(on: int = -1) -> int:
-    """smx_tune_block_pipe: 0 plan every block on the solver stream (the default), 1 plan the
-    next block on a second stream during each sweep (opt-in; the register prefix form after
-    blocks of 12 / 20), 2 the same with the LDS-rolled planner always, -1 query only; returns the
-    previous setting."""
-    return int(load().smx_tune_block_pipe(on))
-
-
-def tune_block_pipe_cus(cus_per_xcd: int = -1, parts: int = -1) -> int:
-    """smx_tune_block_pipe_cus: the CU partition of pipelined chains -- the planner on
-    ``cus_per_xcd`` CUs of every XCD (0: unpartitioned, the default), the sweeps on the rest;
-    ``parts`` > 0 caps the planner's workgroups (0: blk_parts_of); -1 keeps a setting.  Returns
-    the previous cus_per_xcd (-1: out of range, nothing changed)."""
-    return int(load().smx_tune_block_pipe_cus(cus_per_xcd, parts))
 
 
 def tune_shard_xchg(mode: int = -2) -> int:

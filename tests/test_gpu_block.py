@@ -1,6 +1,7 @@
 """GPU parity of block pivots (smx_block_run, csrc/smx_block.hpp): P pivots planned from the
-block's input table and applied in one HBM sweep; every test runs with the planner as one launch
-per pivot and as one persistent launch per block (csrc/smx_plan.hpp).  Bit-exact against the golden fixtures, the C
+block's input table and applied in one HBM sweep; every test runs with both planners: the window
+planner (the default: the first columns of every row kept current step by step, k_blk_wstep) and
+the register-form chains (k_blk_step<L>).  Bit-exact against the golden fixtures, the C
 oracle and the one-pivot-per-sweep chain, for block sizes 1..24, both sweep layouts (pivot-row
 slices in registers / in LDS, smx_tune_block_form), ragged last blocks, terminal outcomes inside
 a block, the x-history ring and interleaving with host steps.
@@ -22,14 +23,14 @@ def _need_gpu():
         pytest.skip("needs an MI355X")
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["launch", "persist"])
+@pytest.fixture(autouse=True, params=[0, 1], ids=["window", "register"])
 def planner_form(request):
-    """Every test twice: the planner as one launch per pivot (k_blk_step) and as one persistent
-    launch per block (k_blk_plan, smx_tune_block_persist) -- the same bits either way."""
+    """Every test twice: the window planner (k_blk_wstep, the default) and the register-form
+    chains (k_blk_step<L>, smx_tune_block_planner(1)) -- the same bits either way."""
     from simplex_mi355x import _lib
-    prev = _lib.tune_block_persist(request.param)
+    prev = _lib.tune_block_planner(request.param, 0)
     yield request.param
-    _lib.tune_block_persist(prev)
+    _lib.tune_block_planner(prev, 0)
 
 
 @pytest.fixture
@@ -88,6 +89,62 @@ def test_every_fixture_block_vs_chain_vs_reference(block_mode, sweep_form, P, fo
         if rec["outcome"]["kind"] in ("optimum", "error"):
             assert a[3] == rec["steps"][-1]["hash"], label
     assert n_blk > 250
+
+
+@pytest.mark.parametrize("P,nwin", [(3, 2), (8, 2), (5, 4), (12, 9)])
+def test_every_fixture_small_window(block_mode, planner_form, P, nwin):
+    """The window planner with a window of a few columns (the first nwin - 1 and the "-b" column):
+    entering, phase-1 and pivot columns past it take the fallbacks (win_colvals / win_chain from
+    the block's input table) -- every trajectory fixture still equals the one-pivot chain and the
+    reference's pivots."""
+    from simplex_mi355x import _lib
+    if planner_form != 0:
+        pytest.skip("window planner only")
+    _lib.tune_block_planner(0, nwin)
+    n_blk = 0
+    for label, cons, func, rec in CASES:
+        if len(func) not in (len(cons[0]) - 1, len(cons[0])) or len(func) < 2:
+            continue
+        cap = trajectory_cap(rec)
+        block_mode(P)
+        sm, a = _solve(cons, func, cap, 7)
+        n_blk += sm._dev.block_plan() is not None
+        block_mode(1)
+        _, b = _solve(cons, func, cap, 7)
+        assert a == b, label
+        exp = [(s["i"], s["j"]) for s in rec["steps"] if "i" in s and s["i"] is not None]
+        assert a[0] == exp[:len(a[0])], label
+    assert n_blk > 250
+
+
+@pytest.mark.parametrize("nwin", [2, 3, 17])
+@pytest.mark.parametrize("kind,n,m,k,chunk,P", [
+    ("uniform", 1023, 1023, 120, 60, 12),
+    ("mixed", 700, 900, 200, 61, 7),           # phase 1: first positive past the window
+    ("degenerate", 511, 511, 150, 75, 8),
+    ("degenerate_mixed", 600, 300, 150, 75, 6),
+    ("mixed", 255, 4095, 60, 60, 20),
+])
+def test_window_fallbacks_vs_oracle(block_mode, planner_form, kind, n, m, k, chunk, P, nwin):
+    """Window planner, small windows on BASELINE-shaped generators: pivots and the whole table bit
+    for bit against the C oracle whichever columns fall outside the window."""
+    from oracle import c_oracle
+    from simplex_mi355x import _lib, lp
+    import simplex
+    if planner_form != 0:
+        pytest.skip("window planner only")
+    _lib.tune_block_planner(0, nwin)
+    block_mode(P)
+    T = lp.dense_tableau(kind, 13, n, m)
+    sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())
+    assert sm._dev.block_plan()[1] == P
+    sm.solve(record_history=False, max_pivots=k, chunk=chunk)
+    Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=8)
+    assert sm.pivots == done
+    assert sm.pivot_log == [tuple(map(int, x)) for x in log]
+    got = sm._dev.download()
+    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
+    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
 
 
 @pytest.mark.parametrize("kind,n,m,k,chunk,P", [
@@ -387,10 +444,9 @@ def test_nofree_knob_with_captured_block_graph():
     assert "nofree ok" in out.stdout
 
 
-def test_persistent_graph_replays_and_tall_fallback(block_mode, planner_form):
-    """The persistent planner's granule tags carry a per-scratch launch count, so replaying ONE
-    captured graph many times never meets a previous replay's records; a table with more rows
-    than planner threads (65,537 > 256 x 256) falls back to one launch per pivot."""
+def test_block_graph_replays_and_tall_table(block_mode, planner_form):
+    """ONE captured graph of a block chain replayed many times continues the trajectory bit for
+    bit; a table with more rows than planner threads (65,537 > 256 x 256 rows)."""
     from oracle import c_oracle
     from simplex_mi355x import lp
     import simplex
