@@ -74,42 +74,46 @@ __device__ __forceinline__ double win_upd(double x, bool prow, bool pcol, double
 }
 
 // The fallback for a column outside the window (and k_blk_prows' whole job): the values of
-// column j after the block's first D pivots, from T_k, step by step.  pr[q] = T_{k+q}[r_q][j]
-// (pivot row q as it was pivoted, q < D) and xo[k] = T_{k+D}[xr[k]][j] for NX more rows.  The
-// pivot rows' own values are carried through the pivots before theirs (a row pivoted twice takes
-// the pivot-row rule at its first step), with the multipliers mul[row][q] = T_{k+q}[row][c_q]
-// that each step stored for every row.
-template <int NX>
+// column j after the block's first D pivots, from T_k, step by step.  out(q, v) receives
+// v = T_{k+q}[r_q][j] (pivot row q as it was pivoted, q < D), and xo[k] = T_{k+D}[xr[k]][j] for NX
+// more rows.  The pivot rows' values are carried through the pivots before theirs (a row pivoted
+// twice takes the pivot-row rule at its first step) with the multipliers mul[row][q] =
+// T_{k+q}[row][c_q] that each step stored for every row.  A rolled loop over the pivots with the
+// rows in a shift register (x[0] is always the next pivot row's value), so the code stays one
+// step's worth (the fully unrolled triangle made the planner kernel ~57 k instructions and its
+// launches instruction-fetch bound: 18.7 us per step, profiles/r06c/).
+template <int NX, class OUT>
 __device__ __forceinline__ void win_colvals(const double* __restrict__ T, int64_t ld, int j,
                                             int D, const BlkPiv& pv,
                                             const double* __restrict__ mul, const int* xr,
-                                            double* pr, double* xo) {
-    double x[kBlkMax + (NX > 0 ? NX : 1)];
+                                            OUT out, double* xo) {
+    double x[kBlkMax];
+    double xx[NX > 0 ? NX : 1];
 #pragma unroll
     for (int p = 0; p < kBlkMax; ++p) x[p] = p < D ? T[(int64_t)pv.r[p] * ld + j] : 0.0;
 #pragma unroll
-    for (int k = 0; k < NX; ++k) x[kBlkMax + k] = T[(int64_t)xr[k] * ld + j];
+    for (int k = 0; k < NX; ++k) xx[k] = T[(int64_t)xr[k] * ld + j];
+#pragma unroll 1
+    for (int q = 0; q < D; ++q) {
+        const double p = x[0];   // T_{k+q}[r_q][j]: updated by the q pivots before it
+        out(q, p);
+        const int rq = pv.r[q];
+        const bool pc = j == pv.c[q];
+        const double e = pv.e[q];
 #pragma unroll
-    for (int q = 0; q < kBlkMax; ++q) {
-        if (q < D) {
-            const double p = x[q];   // T_{k+q}[r_q][j]: updated by the q pivots before it
-            pr[q] = p;
-            const int rq = pv.r[q];
-            const bool pc = j == pv.c[q];
-            const double e = pv.e[q];
-#pragma unroll
-            for (int s = q + 1; s < kBlkMax; ++s)
-                if (s < D)
-                    x[s] = win_upd(x[s], pv.r[s] == rq, pc, p, mul[(int64_t)pv.r[s] * kBlkMax + q],
-                                   e);
-#pragma unroll
-            for (int k = 0; k < NX; ++k)
-                x[kBlkMax + k] = win_upd(x[kBlkMax + k], xr[k] == rq, pc, p,
-                                         mul[(int64_t)xr[k] * kBlkMax + q], e);
+        for (int s = 1; s < kBlkMax; ++s) {
+            const int t = q + s;   // the row of pivot t, not pivoted yet
+            if (t < D)
+                x[s] = win_upd(x[s], pv.r[t] == rq, pc, p, mul[(int64_t)pv.r[t] * kBlkMax + q], e);
         }
+#pragma unroll
+        for (int k = 0; k < NX; ++k)
+            xx[k] = win_upd(xx[k], xr[k] == rq, pc, p, mul[(int64_t)xr[k] * kBlkMax + q], e);
+#pragma unroll
+        for (int s = 0; s + 1 < kBlkMax; ++s) x[s] = x[s + 1];
     }
 #pragma unroll
-    for (int k = 0; k < NX; ++k) xo[k] = x[kBlkMax + k];
+    for (int k = 0; k < NX; ++k) xo[k] = xx[k];
 }
 
 // T_{k+D}[i][j] from T_k through the first D pivots, pj[q] = T_{k+q}[r_q][j] (win_colvals)
@@ -117,11 +121,9 @@ __device__ __forceinline__ double win_chain(const double* __restrict__ T, int64_
                                             int D, const BlkPiv& pv, const double* pj,
                                             const double* __restrict__ mul) {
     double x = T[(int64_t)i * ld + j];
-#pragma unroll
-    for (int q = 0; q < kBlkMax; ++q)
-        if (q < D)
-            x = win_upd(x, i == pv.r[q], j == pv.c[q], pj[q], mul[(int64_t)i * kBlkMax + q],
-                        pv.e[q]);
+#pragma unroll 1
+    for (int q = 0; q < D; ++q)
+        x = win_upd(x, i == pv.r[q], j == pv.c[q], pj[q], mul[(int64_t)i * kBlkMax + q], pv.e[q]);
     return x;
 }
 
@@ -254,9 +256,9 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
                 const int j = j0 + tid;
                 int mine = SMX_NONE;
                 if (j < m) {
-                    double prj[kBlkMax], xo[1];
+                    double xo[1];
                     const int xr[1] = {r};
-                    win_colvals<1>(T, ld, j, D, s_pv, mul, xr, prj, xo);
+                    win_colvals<1>(T, ld, j, D, s_pv, mul, xr, [](int, double) {}, xo);
                     if (xo[0] > 0.0) mine = j;
                 }
                 p1 = block_min_int_dpp<kBlkNT>(mine, s_tmp);
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         if (tid == 0) {
             const int xr[2] = {r, rows};
             double xo[2];
-            win_colvals<2>(T, ld, c, D, s_pv, mul, xr, s_colc, xo);
+            win_colvals<2>(T, ld, c, D, s_pv, mul, xr, [&](int q, double v) { s_colc[q] = v; }, xo);
             s_e = xo[0];
             s_fc = xo[1];
         }
@@ -301,9 +303,9 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
                 const int j = j0 + tid;
                 int mine = SMX_NONE;
                 if (j < fscan) {
-                    double prj[kBlkMax], xo[2];
+                    double xo[2];
                     const int xr[2] = {r, rows};
-                    win_colvals<2>(T, ld, j, D, s_pv, mul, xr, prj, xo);
+                    win_colvals<2>(T, ld, j, D, s_pv, mul, xr, [](int, double) {}, xo);
                     if (win_upd(xo[1], false, j == c, xo[0], fc, e) < 0.0) mine = j;
                 }
                 cf = block_min_int_dpp<kBlkNT>(mine, s_tmp);
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         if (tid == 0) {
             const int xr[1] = {r};
             double xo[1];
-            win_colvals<1>(T, ld, cf, D, s_pv, mul, xr, s_colf, xo);
+            win_colvals<1>(T, ld, cf, D, s_pv, mul, xr, [&](int q, double v) { s_colf[q] = v; }, xo);
             s_prcf = xo[0];
         }
         __syncthreads();
@@ -415,11 +417,8 @@ __global__ __launch_bounds__(kUpdBlock) void k_blk_prows(const double* __restric
     const int C = m + 1;
     const int nt = (int)gridDim.x * kUpdBlock;
     for (int j = (int)blockIdx.x * kUpdBlock + threadIdx.x; j < C; j += nt) {
-        double prj[kBlkMax];
-        win_colvals<0>(T, ld, j, peff, s_pv, mul, nullptr, prj, nullptr);
-#pragma unroll
-        for (int q = 0; q < kBlkMax; ++q)
-            if (q < peff) pr[(int64_t)q * ld + j] = prj[q];
+        win_colvals<0>(T, ld, j, peff, s_pv, mul, nullptr,
+                       [&](int q, double v) { pr[(int64_t)q * ld + j] = v; }, nullptr);
     }
     if (peff != P) return;
     int32_t* fl = blk_rflags(mul, rows + 1);
