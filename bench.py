@@ -6,12 +6,13 @@ the origin so the trajectory is a long phase-2 run), resident in HBM before timi
 A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): its selection
 (pick_element, :70-141) and its Jordan step over every element (recalculate_matrix, :143-177).
 At N = 1 on this table the steps run as block pivots: up to P pivots (the library's policy,
-smx_tune_block: 20 for tables of 1-4 GiB such as this one's 2 GiB, 12 from 256 MiB and beyond
-4 GiB, 10 from 48 MiB) are decided by one planner launch each (k_blk_step, every value of the
-intermediate tables re-derived from the block's input with the update's own expression) and
-applied by ONE sweep of the tableau (k_blk_sweep), so a sweep moves 16 B per element for P pivots
-(a chain of k pivots is cut into blocks of near-equal size: the driver's 20 pivots are ONE sweep
-of 20, the default 200 ten); bit-identical to one pivot per sweep.  After the timed region the
+smx_tune_block: 20 from 1 GiB -- this table's 2 GiB and config 5's 17 GB --, 12 from 256 MiB,
+10 from 48 MiB) are decided by one planner launch each (k_blk_wstep: the window planner keeps the
+first columns of every row current pivot by pivot, csrc/smx_window.hpp), the pivot rows at every
+column are derived once per block (k_blk_prows), and ONE sweep of the tableau (k_blk_sweep)
+applies all of them, so a sweep moves 16 B per element for P pivots (a chain of k pivots is cut
+into blocks of near-equal size: the driver's 20 pivots are ONE sweep of 20, the default 200 ten);
+bit-identical to one pivot per sweep.  After the timed region the
 line adds `sustained` (the next 200 pivots, HIP events around every sweep: the steady-state rate
 beside the burst) and times the one-pivot chain (k_update<kFused>, one kernel per pivot) as
 "single_pivot_update".
@@ -33,10 +34,15 @@ inter-kernel gaps count as kernel time; N > 1: events around every update kernel
 the committed rocprofv3 PMC summary (profiles/), FETCH_SIZE doubled per the gfx950 correction.
 cpu_baseline: the numpy restatement of the same pivot (oracle/numpy_oracle.py, bit-identical to
 the reference) on the same tableau, single thread, a bounded number of pivots.
+parity: after the timed region the line checks itself against the C oracle's run of the same LP
+(tests/golden/bench16k.json, made in the build container by tests/golden/make_bench16k.py): every
+pivot (r, c) so far, and the SHA-256 of the whole table when the line stops at a pivot count the
+fixture hashes (25 = the driver's --warmup 5 --steps 20; 220 = the defaults).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -138,6 +144,18 @@ def load_valu(workload):
             return float(json.load(fh)[workload]["instr_per_element_pivot"])
     except Exception:
         return None
+
+
+def load_clock(workload):
+    """The shader clock (GHz) the dominant sweep runs at, from a committed rocprofv3 GRBM pass
+    (profiles/sweep_clock.json: GRBM_GUI_ACTIVE summed over the 8 XCDs / 8 / the dispatch's
+    duration, written by tools/sweep_clock.py)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "sweep_clock.json")) as fh:
+            rec = json.load(fh)[workload]
+        return float(rec["clock_ghz"]), rec.get("source")
+    except Exception:
+        return None, None
 
 
 def two_term(R, C, pivots_per_launch, instr, avg_kernel, hbm_bytes):
@@ -335,6 +353,39 @@ def sustained_record(dev, P, k, idle_s=1.0):
     return out
 
 
+BENCH_FIXTURE = os.path.join(REPO, "tests", "golden", "bench16k.json")
+
+
+def table_sha256(T, n, m):
+    """SHA-256 of rows 0..n-1 (m + 1 values each, C order) then the f-row's first m values: the
+    hash of tests/golden/make_config5.table_sha256."""
+    import numpy as np
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(T[:n, :m + 1]))
+    h.update(np.ascontiguousarray(T[n, :m]))
+    return h.hexdigest()
+
+
+def parity_check(dev, args, n, m, done):
+    """The line against the C oracle's run of the same LP: the pivots logged
+    so far and, at a pivot count the fixture hashes, the whole table.  None when the workload is
+    not the fixture's (another size, generator or seed)."""
+    if not os.path.exists(BENCH_FIXTURE):
+        return None
+    with open(BENCH_FIXTURE) as fh:
+        fx = json.load(fh)
+    if (n, m, args.kind, args.seed) != (fx["n"], fx["m"], fx["kind"], fx["seed"]):
+        return None
+    k = min(done, int(fx["pivots"]))
+    log_ok = dev.read_log(0, k).tolist() == fx["log"][:k]
+    sha_ok = None
+    if str(done) in fx["sha256"]:
+        sha_ok = table_sha256(dev.download(), n, m) == fx["sha256"][str(done)]
+    return {"ok": bool(log_ok and sha_ok is not False), "pivots_checked": k,
+            "log_equal": bool(log_ok), "sha256_at": done if sha_ok is not None else None,
+            "sha256_equal": sha_ok, "fixture": "tests/golden/bench16k.json (C oracle)"}
+
+
 def run_single(args):
     import numpy as np
     import torch
@@ -385,6 +436,15 @@ def run_single(args):
         if instr is not None:
             extra["two_term"] = two_term(R, C, args.steps / len(sw), instr, avg_kernel,
                                          bytes_per_sweep)
+            ghz, src = load_clock(f"{R}x{C}/{kernel}")
+            if ghz is not None:
+                # the VALU term at the clock the sweep actually holds (power-managed)
+                tt = extra["two_term"]
+                t_clk = tt["wave_instr_per_launch"] / (tt["cus"] * ghz * 1e9)
+                tt["clock_ghz"] = ghz
+                tt["clock_source"] = src
+                tt["valu_ms_at_clock"] = t_clk * 1e3
+                tt["valu_frac_at_clock"] = t_clk / avg_kernel
         # every launch of the chain: k_blk_start, per block Pb k_blk_step and k_blk_sweep +
         # k_blk_sweep_rest (the last one also publishes the chain's state)
         kernels_per_pivot = (args.steps + 2 * len(sw) + 1) / args.steps
@@ -424,6 +484,7 @@ def run_single(args):
     done = int(ctl["npivots"])
     valid = done == args.warmup + args.steps and not ctl["term"]
     cycle = cycle_report(n, m, dev.read_log(0, done))
+    parity = parity_check(dev, args, n, m, done)
     if resident is not None:
         # algorithmic bytes of a chain held in LDS: not an HBM rate, no physical bound applies
         achieved = bytes_per_sweep / avg_kernel / 1e9
@@ -463,7 +524,10 @@ def run_single(args):
         "equiv_one_pass_note": "16 B/element/pivot over wall time per pivot; a block sweep "
                                "moves 16 B/element once per P pivots, so this is not HBM traffic",
         "device_ms_per_step": dev_ms / args.steps,
-        "roofline": dict({"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+        "parity": None if parity is None else parity["ok"],
+        "parity_detail": parity,
+        "roofline": dict({"bound": (extra.get("two_term") or {}).get("bound", "hbm"),
+                          "achieved": achieved, "peak": PEAK_HBM_GBS,
                           "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                           "kernel": kernel, "algorithmic_bytes_per_launch": bytes_per_sweep,
                           "avg_kernel_ms": avg_kernel * 1e3,
@@ -481,8 +545,28 @@ def run_single(args):
     print(json.dumps(out), flush=True)
 
 
+def check_world(args, env=None):
+    """--gpus N must match the world torch.distributed.run formed: a bare
+    `python bench.py --gpus 8` would otherwise run one rank and print an n_gpus 1 line.  Runs
+    before anything touches the GPU; returns an error message or None."""
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in env and args.gpus > 1:
+        return (f"bench.py --gpus {args.gpus}: launch one rank per GPU with `python -m "
+                f"torch.distributed.run --nnodes=1 --nproc-per-node {args.gpus} --master-addr "
+                f"127.0.0.1 --master-port <port> bench.py --gpus {args.gpus} ...`")
+    if world != args.gpus:
+        return (f"bench.py --gpus {args.gpus} but torch.distributed.run formed WORLD_SIZE={world}: "
+                "refusing to report a line for a different GPU count")
+    return None
+
+
 def main():
     args = parse()
+    msg = check_world(args)
+    if msg:
+        print(msg, file=sys.stderr, flush=True)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1 or args.sharded:
         from simplex_mi355x import sharded

@@ -198,3 +198,78 @@ def test_forced_record_agrees_with_rocprof():
         rec = [json.loads(ln) for ln in fh if '"forced_update_us"' in ln and '"size": 8192' in ln][0]
     prof_us = _rocprof_avg_ms("r04a/kernel_stats_run_configs3.csv", "k_update<2,") * 1e3
     assert abs(rec["forced_update_us"] - prof_us) / prof_us < 0.05, (rec, prof_us)
+
+
+def test_world_guard_refuses_a_bare_multi_gpu_launch():
+    """`python bench.py --gpus 2` without torch.distributed.run exits non-zero before touching the
+    GPU (it used to fall into the sharded path at WORLD_SIZE 1 and print an n_gpus 1 line), and a
+    torchrun world that differs from --gpus is refused too."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"],
+                         capture_output=True, text=True, timeout=120, env=env, cwd=REPO)
+    assert out.returncode == 2, out
+    assert "torch.distributed.run" in out.stderr
+    bench = _bench_module()
+
+    class A:
+        gpus = 4
+    assert bench.check_world(A(), {"WORLD_SIZE": "2"}) is not None
+    assert bench.check_world(A(), {"WORLD_SIZE": "4"}) is None
+    A.gpus = 1
+    assert bench.check_world(A(), {}) is None
+
+
+def test_parity_check_against_the_bench_fixture():
+    """bench.parity_check: the line's own pivots (and, at 25 / 220 pivots, the table's SHA-256)
+    against tests/golden/bench16k.json (the C oracle's run of the bench LP); a wrong pivot or a
+    wrong table fails it, another workload is not checked."""
+    import numpy as np
+    bench = _bench_module()
+    with open(os.path.join(REPO, "tests", "golden", "bench16k.json")) as fh:
+        fx = json.load(fh)
+    assert fx["n"] == fx["m"] == 16383 and fx["kind"] == "uniform" and fx["seed"] == 0
+    assert set(fx["sha256"]) >= {"25", "220"} and len(fx["log"]) == fx["pivots"] >= 220
+
+    class Dev:
+        def __init__(self, log, table=None):
+            self._log, self._t = np.array(log, dtype=np.int32), table
+
+        def read_log(self, a, b):
+            return self._log[a:b]
+
+        def download(self):
+            return self._t
+
+    class A:
+        kind, seed = "uniform", 0
+    ok = bench.parity_check(Dev(fx["log"][:30]), A(), 16383, 16383, 30)
+    assert ok["ok"] and ok["pivots_checked"] == 30 and ok["sha256_equal"] is None
+    bad = [list(x) for x in fx["log"][:30]]
+    bad[7][1] += 1
+    assert bench.parity_check(Dev(bad), A(), 16383, 16383, 30)["ok"] is False
+    # at 25 pivots the table is hashed: a wrong table fails (a small stand-in table)
+    wrong = np.zeros((16384, 16384), dtype=np.float64)
+    r = bench.parity_check(Dev(fx["log"][:25], wrong), A(), 16383, 16383, 25)
+    assert r["sha256_at"] == 25 and r["sha256_equal"] is False and r["ok"] is False
+    assert bench.parity_check(Dev([]), A(), 8191, 8191, 0) is None
+    # the hash is the fixture generator's
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "mk5", os.path.join(REPO, "tests", "golden", "make_config5.py"))
+    T = np.arange(7 * 5, dtype=np.float64).reshape(7, 5)
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    assert mk.table_sha256(T, 6, 4) == bench.table_sha256(T, 6, 4)
+
+
+def test_roofline_bound_follows_the_two_term_bound():
+    """The block line's roofline.bound is the two-term bound's (fp64 VALU issue for the 20-pivot
+    sweep), with the VALU fraction at the committed shader clock beside it."""
+    import re
+    src = open(os.path.join(REPO, "bench.py")).read()
+    assert re.search(r'"bound": \(extra\.get\("two_term"\) or \{\}\)\.get\("bound", "hbm"\)', src)
+    bench = _bench_module()
+    ghz, source = bench.load_clock("16384x16384/k_blk_sweep<20>")
+    assert ghz is not None and 1.0 < ghz < 2.5 and source
