@@ -485,6 +485,10 @@ typedef struct smx_rank {
 int smx_mshard_comms(void** comms_out, int32_t nranks, const int32_t* devices);
 int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,
                    int32_t pivots, int32_t exchange);
+/* The first rank's own error of the last smx_mshard_run that returned SMX_ERR_COMMS_ABORTED
+ * (a hipError_t, or -1000 - ncclResult_t), 0 if that call succeeded; *rank_out = that rank's
+ * index (-1: none).  Every failing rank is also reported on stderr. */
+int smx_mshard_last_error(int32_t* rank_out);
 /* smx_mshard_run's k pivots with the copy exchange, every rank on ranks[0]'s device (the host-
  * bound case: ~3N host calls per pivot), captured once as ONE graph on ranks[0].stream -- the
  * other ranks' streams fork from and join back into it, and every event the capture records is

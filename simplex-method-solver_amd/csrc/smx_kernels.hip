@@ -185,6 +185,10 @@ int variant_for(const smx_shape& s) {
 // is resident at once and the balanced unit ranges finish together (no second residency round).
 // The host-side caches below are shared by smx_mshard_run's per-device threads: one mutex.
 std::mutex g_cache_mu;
+// smx_mshard_run (RCCL exchange): the first failing rank's own error code and index, kept for
+// smx_mshard_last_error (the call itself returns SMX_ERR_COMMS_ABORTED after aborting every
+// communicator); guarded by g_cache_mu
+int g_mshard_err = 0, g_mshard_err_rank = -1;
 
 // Resident 256-thread blocks per CU of `fn` by the occupancy API (registers and LDS), one block
 // of margin below its answer, cached; at most `cap`.
@@ -2025,13 +2029,27 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                 errs[(size_t)q] = e;
             });
         for (auto& t : th) t.join();
-        int first = 0;
-        for (int e : errs)
-            if (e && !first) first = e;
+        int first = 0, first_rank = -1;
+        for (int q = 0; q < nranks; ++q) {
+            const int e = errs[(size_t)q];
+            if (!e) continue;
+            // every failing rank's own code, before the abort hides it behind one status
+            fprintf(stderr, "smx_mshard_run: rank %d (device %d) failed: %s %d\n", q,
+                    ranks[q].device, e <= -1000 ? "RCCL" : "hipError", e <= -1000 ? -1000 - e : e);
+            if (!first) {
+                first = e;
+                first_rank = q;
+            }
+        }
+        {
+            std::lock_guard<std::mutex> lock(g_cache_mu);
+            g_mshard_err = first;
+            g_mshard_err_rank = first_rank;
+        }
         if (first) {
             // a rank that failed mid-chain leaves the others' enqueued collectives waiting for
             // it forever: abort every communicator (the caller must not destroy them afterwards,
-            // SMX_ERR_COMMS_ABORTED)
+            // SMX_ERR_COMMS_ABORTED; smx_mshard_last_error returns the first rank's own code)
             for (int q = 0; q < nranks; ++q)
                 (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(ranks[q].comm));
             return SMX_ERR_COMMS_ABORTED;
@@ -2039,6 +2057,12 @@ int smx_mshard_run(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
         return 0;
     }
     return mshard_enqueue(ranks, nranks, parity, k, pivots, exchange);
+}
+
+int smx_mshard_last_error(int32_t* rank_out) {
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    if (rank_out) *rank_out = g_mshard_err_rank;
+    return g_mshard_err;
 }
 
 int smx_mshard_graph_create(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_t k,

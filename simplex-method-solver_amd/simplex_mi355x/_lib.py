@@ -121,7 +121,7 @@ EXPORTS = (
     "smx_bshard_pick", "smx_bshard_step_light", "smx_tune_shard_xchg",
     "smx_host_select", "smx_host_pivot", "smx_host_run", "smx_timer_reserve",
     "smx_mshard_comms", "smx_mshard_run", "smx_int_first_fix", "smx_host_int_first_fix",
-    "smx_diag_path_counts", "smx_comm_info", "smx_mshard_graph_create",
+    "smx_diag_path_counts", "smx_comm_info", "smx_mshard_graph_create", "smx_mshard_last_error",
 )
 
 
@@ -240,6 +240,7 @@ def load():
         "smx_mshard_comms": ([ctypes.POINTER(ctypes.c_void_p), i32, ctypes.POINTER(i32)],
                              ctypes.c_int),
         "smx_mshard_run": ([ctypes.POINTER(Rank), i32, i32, i32, i32, i32], ctypes.c_int),
+        "smx_mshard_last_error": ([ctypes.POINTER(i32)], ctypes.c_int),
         "smx_int_first_fix": ([vp, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp, vp],
                               ctypes.c_int),
         "smx_host_int_first_fix": ([vp, vp, i64, i32, i32, i32, i32, vp, vp, i64, vp],
@@ -342,7 +343,13 @@ def check(err: int, what: str) -> None:
     if err == 0:
         return
     if err == ERR_COMMS_ABORTED:
-        raise RuntimeError(f"{what} failed: a rank could not enqueue its chain; every RCCL "
+        rank = ctypes.c_int32(-1)
+        cause = int(load().smx_mshard_last_error(ctypes.byref(rank)))
+        why = ""
+        if cause:
+            why = (f" (rank {rank.value}: RCCL {NCCL_RESULTS.get(-1000 - cause, -1000 - cause)})"
+                   if cause <= -1000 else f" (rank {rank.value}: hipError {cause})")
+        raise RuntimeError(f"{what} failed: a rank could not enqueue its chain{why}; every RCCL "
                            "communicator was aborted")
     if err <= -1000:
         code = -1000 - err

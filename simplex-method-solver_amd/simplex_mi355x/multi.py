@@ -97,6 +97,7 @@ class MultiTableau:
             _lib.check(L.smx_mshard_comms(comms, P, devs), "smx_mshard_comms")
             self._comms = [comms[p] for p in range(P)]
         self._structs = self._rank_structs()
+        self._aborted = False     # smx_mshard_run aborted the communicators (see _native)
         # opt-in: chained runs of ranks sharing ONE device (copy exchange) replay a captured graph
         # per (parity, k) -- one host call per chain instead of ~3N per pivot
         # (smx_mshard_graph_create); other layouts enqueue eagerly
@@ -139,11 +140,19 @@ class MultiTableau:
                 g = self._graphs[key] = Graph(h.value)
             g.launch(self.ranks[0].dev.stream.cuda_stream)
             return
+        if self._aborted:
+            raise RuntimeError("MultiTableau: its RCCL communicators were aborted by an earlier "
+                               "failed run; build a new MultiTableau")
         err = _lib.load().smx_mshard_run(
             self._structs, self.world, self.step & 1, int(k), int(pivots),
             _lib.XCHG_RCCL if self.exchange == "rccl" else _lib.XCHG_COPY)
         if err == _lib.ERR_COMMS_ABORTED:
-            self._comms = None   # aborted by the library: nothing left to destroy
+            # aborted (and freed) by the library: no handle may reach RCCL again -- not through
+            # the rank table either (a later run() passed the freed handles)
+            self._comms = None
+            for p in range(self.world):
+                self._structs[p].comm = None
+            self._aborted = True
         _lib.check(err, "smx_mshard_run")
 
     def _sync(self) -> None:
