@@ -177,6 +177,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     // Everything that does not depend on the decision is loaded with the decision's operands
     // (one round trip): the stop flag, the pivots so far, the f-row's window, this wave's first
     // rows.  On a stopped chain those loads read stale scratch and are discarded.
+    SMX_BLK_STAMP(0);
     const int stopped = ctl->term;
     blk_load_pivots(h, D, &s_pv);
     const double fo = jl >= 0 ? Wo[(int64_t)rows * kWin + lane] : 0.0;
@@ -220,6 +221,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         }
     }
     __syncthreads();
+    SMX_BLK_STAMP(1);
     if (stopped) {
         if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
         return;
@@ -291,6 +293,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         e = s_e;
         fc = s_fc;
     }
+    SMX_BLK_STAMP(2);
     // the f-row after this pivot (never the pivot row) and the next entering column: first
     // j < fscan with f_{k+L}[j] < 0 (simplex.py:94-98)
     const double fn = jl >= 0 ? win_upd(fo, false, jl == c, pw, fc, e) : 0.0;
@@ -312,6 +315,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
             }
         }
     }
+    SMX_BLK_STAMP(3);
     const int cfs = __builtin_amdgcn_readfirstlane(cf != SMX_NONE ? win_slot(cf, nwin, C) : -1);
     if (cf != SMX_NONE && cfs < 0) {
         // the records' column outside the window: the pivot rows there, T_{k+D}[r][cf] too
@@ -355,6 +359,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         }
     }
     if (b == 0 && wid == 0 && jl >= 0) Wn[(int64_t)rows * kWin + lane] = fn;
+    SMX_BLK_STAMP(4);
     const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
     const bool want_x = xhist && log_cap > 0;
     // the row pass: every row of the wave through this pivot at the window's columns, its
@@ -398,7 +403,9 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
             blk_rec_add(R, i, bv, cf != SMX_NONE, a);
         }
     }
+    SMX_BLK_STAMP(5);
     win_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);
+    SMX_BLK_STAMP(7);
 }
 
 // After a block's last planner step: the pivot rows at every column, pr[q][j] = T_{k+q}[r_q][j]

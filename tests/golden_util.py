@@ -61,6 +61,15 @@ def dense_hash(T: np.ndarray, n: int, flen: int) -> str:
     return h.hexdigest()
 
 
+def table_sha256(T: np.ndarray, n: int, m: int) -> str:
+    """SHA-256 of a dense tableau as the full-size fixtures hash it (tests/golden/make_config5.py,
+    make_bench16k.py): rows 0..n-1 with m + 1 values each in C order, then the f-row's first m."""
+    h = hashlib.sha256()
+    h.update(np.ascontiguousarray(T[:n, :m + 1]))
+    h.update(np.ascontiguousarray(T[n, :m]))
+    return h.hexdigest()
+
+
 def same_value(a, b, signed_zero=True) -> bool:
     """Bitwise float equality (NaN == NaN; -0.0 != 0.0 unless signed_zero=False)."""
     if isinstance(a, int) and isinstance(b, int):

@@ -3,9 +3,11 @@
 * config 4 -- a 16384 x 16384 tableau row-sharded over 2 and then 4 ranks (block pivots, 8 per
   sweep, and the one-pivot fused protocol), bit for bit against the unsharded C oracle over a
   prefix with a ragged last block;
-* config 5 -- a 65536 x 32768 degenerate tableau (both degenerate generators) row-sharded over
-  8 ranks on the block path: a 9-pivot prefix bit for bit against the C oracle, then 200 pivots
-  whose trajectory, cycle report and final table are identical to the unsharded HIP path.
+* config 5 -- a 65536 x 32768 degenerate tableau (both degenerate generators), the unsharded HIP
+  path against the C oracle AT FULL SIZE over 209 pivots through the committed fixture
+  tests/golden/config5.json (made in the build container by tests/golden/make_config5.py: the
+  oracle's pivot log, its basis-cycle report and the table's SHA-256 after pivots 20, 60, 140 and
+  209), and the same chain row-sharded over 8 ranks identical to it, row by row.
 
 The ranks are simulated in one process on the one GPU of the test box: every rank is its own
 ``BlockShardBackend`` / ``HipShardBackend`` (own buffers, own stream), the all-gather is a device
@@ -124,58 +126,55 @@ def test_config4_one_pivot_sharded_16k(table16k, world):
 
 # ----------------------------------------------------------------------------------------------
 # config 5: 65536 x 32768 row-sharded across 8 ranks, degenerate / anti-cycling stress
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("kind", ["degenerate", "degenerate_mixed"])
 def test_config5_sharded_65536x32768(kind):
+    """The unsharded block chain (20 pivots per sweep, the window planner) against the C oracle's
+    full-size run (fixture): every pivot, the cycle report, the whole table after 20, 60, 140 and
+    209 pivots; 8 simulated ranks (8 pivots per sweep, the register planner and the exchange of
+    the multi-GPU run) identical to it after 9 and 209 pivots."""
+    from golden_util import load, table_sha256
     from simplex_mi355x import lp
     from simplex_mi355x.device import DeviceTableau
-    from oracle import c_oracle
     from test_gpu_block_sharded import _backends, _lockstep
+    fx = [c for c in load("config5.json")["cases"] if c["kind"] == kind][0]
     n, m, world, P = 65535, 32767, 8, 8
+    assert (fx["n"], fx["m"], fx["seed"]) == (n, m, 0)
     T = lp.dense_tableau(kind, 0, n, m)
     dev = DeviceTableau(T, n, m, m, log_cap=1 << 12)
     assert dev.block_plan()[1] == 20           # the unsharded path: up to 20 pivots per sweep (8 GiB)
     bes = _backends(T, n, m, world, P)
-
-    # 9-pivot prefix (sharded: a block of 8 + a ragged 1; unsharded: one block) against the C
-    # oracle, bit for bit
-    k0 = 9
-    Tref, st, done, log = c_oracle.run(T, n, m, m, k0, threads=16)
     del T
     gc.collect()
-    dev.run(k0, graph=False)
-    ctl = dev.sync_state()
-    _lockstep(bes, k0, P)
-    assert int(ctl["npivots"]) == done, (int(ctl["npivots"]), done, st)
-    assert np.array_equal(dev.read_log(0, done), log)
+    done = 0
+    for stop in (9, 20, 60, 140, fx["pivots"]):
+        dev.run(stop - done, graph=False)
+        ctl = dev.sync_state()
+        assert int(ctl["npivots"]) == stop and not ctl["term"], (stop, int(ctl["npivots"]))
+        if stop == 9:
+            _lockstep(bes, 9, P)
+        elif stop == fx["pivots"]:
+            _lockstep(bes, stop - 9, P)
+        done = stop
+        assert dev.read_log(0, stop).tolist() == fx["log"][:stop], stop
+        if str(stop) in fx["sha256"]:
+            got = dev.download()
+            assert table_sha256(got, n, m) == fx["sha256"][str(stop)], stop
+            del got
+            gc.collect()
+        if stop == 9:
+            for be in bes:
+                assert be.state()["npivots"] == 9
+                assert be.log(0, 9).tolist() == fx["log"][:9]
+            _rows_equal_on_device(bes, dev, n, m)
+    total = fx["pivots"]
+    cyc = _cycle(n, m, dev.read_log(0, total))
+    assert (list(cyc) if cyc else None) == fx["cycle"]
     for be in bes:
         s = be.state()
-        assert s["npivots"] == done
-        assert np.array_equal(be.log(0, done), log)
-    got = dev.download()
-    assert np.array_equal(got[:n].view(np.int64), Tref[:n].view(np.int64))
-    assert np.array_equal(got[n, :m].view(np.int64), Tref[n, :m].view(np.int64))
-    del got, Tref
-    gc.collect()
+        assert s["npivots"] == total and not s["term"]
+        assert be.log(0, total).tolist() == fx["log"]
     _rows_equal_on_device(bes, dev, n, m)
-
-    # 200 more pivots: identical trajectory, cycle report and table as the unsharded HIP path
-    k1 = 200
-    dev.run(k1, graph=False)
-    ctl = dev.sync_state()
-    _lockstep(bes, k1, P)
-    total = int(ctl["npivots"])
-    ref_log = dev.read_log(0, total)
-    for be in bes:
-        s = be.state()
-        assert s["npivots"] == total and s["term"] == bool(ctl["term"])
-        if s["term"]:
-            assert s["status"] == int(ctl["sel_status"])
-        assert np.array_equal(be.log(0, total), ref_log)
-    assert total == k0 + k1 or bool(ctl["term"])
-    cyc = _cycle(n, m, ref_log)
-    assert _cycle(n, m, bes[0].log(0, total)) == cyc
-    _rows_equal_on_device(bes, dev, n, m)
-    print(f"config 5 ({kind}): {total} pivots, basis cycle {cyc}")
+    print(f"config 5 ({kind}): {total} pivots, basis cycle {cyc} = the oracle's")
     del bes, dev
     _free()

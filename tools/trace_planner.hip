@@ -8,7 +8,7 @@
 // Build (from the repo root):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DSMX_BLK_TRACE -Iinclude \
 //     -I/opt/rocm/include -L/opt/rocm/lib -lrccl tools/trace_planner.hip -o tools/trace_planner
-// Run: tools/trace_planner [N] [P] [blocks]
+// Run: tools/trace_planner [N] [P] [blocks] [planner: 0 window (default), 1 register]
 #include "../simplex-method-solver_amd/csrc/smx_kernels.hip"
 
 #include <algorithm>
@@ -46,6 +46,7 @@ int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 16384;
     const int P = argc > 2 ? atoi(argv[2]) : 12;
     const int nblocks = argc > 3 ? atoi(argv[3]) : 3;
+    if (argc > 4) smx_tune_block_planner(atoi(argv[4]), 0);
     smx_shape s{};
     s.m = N - 1;
     s.n = s.rows = N - 1;
@@ -79,13 +80,20 @@ int main(int argc, char** argv) {
         parity = (parity + P) & 1;
         static unsigned long long tr[kBlkMax + 1][kBlkTraceParts][8];
         CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_blk_trace), sizeof(tr)));
+        {
+            static const unsigned long long z[kBlkMax + 1][kBlkTraceParts][8] = {};
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_blk_trace), z, sizeof(z)));
+        }
         static unsigned fb[kBlkMax + 1][2];
         CK(hipMemcpyFromSymbol(fb, HIP_SYMBOL(g_blk_fallback), sizeof(fb)));
         {
             static const unsigned zero[kBlkMax + 1][2] = {};
             CK(hipMemcpyToSymbol(HIP_SYMBOL(g_blk_fallback), zero, sizeof(zero)));
         }
-        const int G = s.nparts < kBlkTraceParts ? s.nparts : kBlkTraceParts;
+        // the first kBlkTraceParts planner workgroups (window planner: phases 0 entry, 1 decision,
+        // 2 pivot element, 3 next entering column, 4 bookkeeping, 5 row pass, 7 records stored)
+        const int Gp = g_block_planner == 0 ? win_groups(s.rows) : blk_parts_of(s.nparts, s.rows);
+        const int G = Gp < kBlkTraceParts ? Gp : kBlkTraceParts;
         unsigned long long prev_end = 0;
         for (int L = 1; L <= P; ++L) {
             unsigned long long t0 = ~0ull, tend = 0;
@@ -101,7 +109,9 @@ int main(int argc, char** argv) {
                    rep, N, P, L, (tend - t0) * 0.01, gap);
             for (int ph = 0; ph < 8; ++ph) {
                 std::vector<double> v;
-                for (int g = 0; g < G; ++g) v.push_back((tr[L][g][ph] - t0) * 0.01);
+                for (int g = 0; g < G; ++g)
+                    if (tr[L][g][ph]) v.push_back((tr[L][g][ph] - t0) * 0.01);
+                if (v.empty()) v.push_back(-1.0);
                 std::sort(v.begin(), v.end());
                 printf("%s%.2f", ph ? ", " : "", v[v.size() / 2]);
             }
