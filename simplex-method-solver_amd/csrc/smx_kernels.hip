@@ -601,9 +601,10 @@ int launch_blk_wstep(int L, const double* T, const smx_shape& s, int P, int pari
 }
 int launch_blk_prows(const double* T, const smx_shape& s, int P, const BlkPtrs& b,
                      hipStream_t st) {
+    // one column per thread, 64-thread workgroups: 16384 columns over all 256 CUs
     const int64_t work = std::max<int64_t>(s.m + 1, s.rows + 1);
-    const int grid = (int)std::min<int64_t>((work + kUpdBlock - 1) / kUpdBlock, num_cus() * 4);
-    hipLaunchKernelGGL(k_blk_prows, dim3(grid), dim3(kUpdBlock), 0, st, T, s.ld, s.rows, s.m, P,
+    const int grid = (int)std::min<int64_t>((work + kProwsNT - 1) / kProwsNT, num_cus() * 8);
+    hipLaunchKernelGGL(k_blk_prows, dim3(grid), dim3(kProwsNT), 0, st, T, s.ld, s.rows, s.m, P,
                        (const BlkHdr*)b.h[0], b.mul[0], b.pr[0]);
     return (int)hipGetLastError();
 }

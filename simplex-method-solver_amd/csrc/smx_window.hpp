@@ -32,7 +32,7 @@ namespace {
 // both planners, and with windows of 2..64 columns to drive the fallbacks).
 // (kWin = 64 window slots per row, one wave's lanes: smx_block.hpp, beside the scratch layout)
 constexpr int kWinMaxG = 256;     // planner workgroups at most (the records merge: kBlkPartsMax)
-constexpr int kWinBatch = 8;      // rows of a wave whose window loads are in flight together
+constexpr int kWinBatch = 8;      // rows of a wave updated together (two batches in flight)
 static_assert(kWinMaxG <= kBlkPartsMax, "window planner records");
 
 // Rows per wave and workgroups of a window step for `rows` constraint rows: four waves per
@@ -127,30 +127,6 @@ __device__ __forceinline__ double win_chain(const double* __restrict__ T, int64_
     return x;
 }
 
-// The merged record of a workgroup's four waves (each wave's BlkRec is uniform across its lanes)
-__device__ __forceinline__ void win_rec_store(const BlkRec& R, smx_part* out) {
-    __shared__ BlkRec s_r[kBlkNT / kWave];
-    const int wid = threadIdx.x >> 6;
-    if ((threadIdx.x & (kWave - 1)) == 0) s_r[wid] = R;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        BlkRec a = s_r[0];
-        for (int w = 1; w < kBlkNT / kWave; ++w) {
-            a.nb = min(a.nb, s_r[w].nb);
-            if (s_r[w].f.idx < a.f.idx) a.f = s_r[w].f;
-            if (better(s_r[w].bc, a.bc)) a.bc = s_r[w].bc;
-        }
-        smx_part pt;
-        pt.p1col = a.nb;
-        pt.first = a.f.idx;
-        pt.first_v = a.f.v;
-        pt.best_cls = a.bc.cls;
-        pt.best_i = a.bc.idx;
-        pt.best_v = a.bc.v;
-        *out = pt;
-    }
-}
-
 // One pivot of the block (step L: decide block step D = L - 1, apply it to the window, build the
 // records of step L).  Grid: win_groups(rows) workgroups of kBlkNT threads; wave w owns
 // constraint rows [w rpw, (w + 1) rpw).  W = the window, [2][rows + 1][kWin] by step parity.
@@ -183,10 +159,14 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     const double fo = jl >= 0 ? Wo[(int64_t)rows * kWin + lane] : 0.0;
     const int i0 = (b * (kBlkNT / kWave) + wid) * rpw;
     const int i1 = min(rows, i0 + rpw);
-    double xv[kWinBatch];
+    // this wave's first two batches of rows (the row pass keeps two batches in flight)
+    double xv[kWinBatch], xn[kWinBatch];
 #pragma unroll
-    for (int u = 0; u < kWinBatch; ++u)
+    for (int u = 0; u < kWinBatch; ++u) {
         xv[u] = (i0 + u < i1 && jl >= 0) ? Wo[(int64_t)(i0 + u) * kWin + lane] : 0.0;
+        xn[u] = (i0 + kWinBatch + u < i1 && jl >= 0)
+                    ? Wo[(int64_t)(i0 + kWinBatch + u) * kWin + lane] : 0.0;
+    }
     if (wid == 0) {
         // the decision of step D from its records (every workgroup, identically)
         const int c = h->cfs[blk_slot(D, P, bn)];
@@ -362,74 +342,150 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     SMX_BLK_STAMP(4);
     const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
     const bool want_x = xhist && log_cap > 0;
-    // the row pass: every row of the wave through this pivot at the window's columns, its
-    // multiplier T_{k+D}[i][c] stored for the sweep, and the records of step L on column cf
+    // The row pass: every row of the wave through this pivot at the window's columns, its
+    // multiplier T_{k+D}[i][c] stored for the sweep, and the records of step L on column cf.
+    // A batch's rows are independent: their multipliers (lane cs), updates and stores are issued
+    // together, then lane u takes row u's "-b" and entering-column entries (ds_bpermute) and adds
+    // it to its own partial record; the wave's partials are reduced once at the end (DPP).  (Row by
+    // row with scalar read-backs and a record update per row, one dependent division chain after
+    // another, the pass took 9.2 us of a 15.3 us step at 16 rows per wave, profiles/r06e/.)
     const int ms = __builtin_amdgcn_readfirstlane(win_slot(m, nwin, C));
     double* __restrict__ mT = blk_mulT(mul, rows + 1);
     BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
     for (int ib = i0; ib < i1; ib += kWinBatch) {
-        if (ib > i0) {
-#pragma unroll
-            for (int u = 0; u < kWinBatch; ++u)
-                xv[u] = (ib + u < i1 && jl >= 0) ? Wo[(int64_t)(ib + u) * kWin + lane] : 0.0;
-        }
         // fallbacks (columns outside the window): lane u derives row ib + u's value from T_k
         double mcv = 0.0, acv = 0.0;
         if (cs < 0 && lane < kWinBatch && ib + lane < i1)
             mcv = win_chain(T, ld, ib + lane, c, D, s_pv, s_colc, mul);
         if (cfs < 0 && cf != SMX_NONE && lane < kWinBatch && ib + lane < i1)
             acv = win_chain(T, ld, ib + lane, cf, D, s_pv, s_colf, mul);
+        double mc[kWinBatch], nv[kWinBatch];
+#pragma unroll
+        for (int u = 0; u < kWinBatch; ++u) mc[u] = __shfl(cs >= 0 ? xv[u] : mcv, cs >= 0 ? cs : u);
+#pragma unroll
+        for (int u = 0; u < kWinBatch; ++u) nv[u] = win_upd(xv[u], ib + u == r, jl == c, pw, mc[u], e);
+#pragma unroll
+        for (int u = 0; u < kWinBatch; ++u)
+            if (ib + u < i1 && jl >= 0) Wn[(int64_t)(ib + u) * kWin + lane] = nv[u];
+        // the next batch in flight while this one's records are built
 #pragma unroll
         for (int u = 0; u < kWinBatch; ++u) {
-            const int i = ib + u;
-            if (i >= i1) break;
-            const double x = xv[u];
-            const double mc = cs >= 0 ? readlane_d(x, cs) : readlane_d(mcv, u);
-            const double nv = win_upd(x, i == r, jl == c, pw, mc, e);
-            if (jl >= 0) Wn[(int64_t)i * kWin + lane] = nv;
-            if (lane == 0) {
-                mul[(int64_t)i * kBlkMax + D] = mc;
-                mT[(int64_t)D * (rows + 1) + i] = mc;
+            xv[u] = xn[u];
+            const int i2 = ib + 2 * kWinBatch + u;
+            if (i2 < i1 && jl >= 0) xn[u] = Wo[(int64_t)i2 * kWin + lane];
+        }
+        double myc = 0.0, mybv = 0.0, mya = 0.0;
+#pragma unroll
+        for (int u = 0; u < kWinBatch; ++u) {
+            const double bvu = __shfl(nv[u], ms);
+            const double au = cfs >= 0 ? __shfl(nv[u], cfs) : 0.0;
+            if (lane == u) {
+                myc = mc[u];
+                mybv = bvu;
+                mya = au;
             }
-            const double bv = readlane_d(nv, ms);
-            double a = 0.0;
-            if (cf != SMX_NONE)
-                a = cfs >= 0 ? readlane_d(nv, cfs)
-                             : win_upd(readlane_d(acv, u), i == r, cf == c, s_prcf, mc, e);
-            if (want_x && lane == 0) {
-                if (i == hx0) xhist[hslot] = bv;
-                if (i == hx1) xhist[hslot + 1] = bv;
+        }
+        const int i = ib + lane;
+        if (lane < kWinBatch && i < i1) {
+            if (cf != SMX_NONE && cfs < 0)
+                mya = win_upd(acv, i == r, cf == c, s_prcf, myc, e);
+            mul[(int64_t)i * kBlkMax + D] = myc;
+            mT[(int64_t)D * (rows + 1) + i] = myc;
+            if (want_x) {
+                if (i == hx0) xhist[hslot] = mybv;
+                if (i == hx1) xhist[hslot + 1] = mybv;
             }
-            blk_rec_add(R, i, bv, cf != SMX_NONE, a);
+            blk_rec_add(R, i, mybv, cf != SMX_NONE, mya);
         }
     }
     SMX_BLK_STAMP(5);
-    win_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);
+    blk_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);   // DPP per wave, then the 4 waves
     SMX_BLK_STAMP(7);
 }
 
 // After a block's last planner step: the pivot rows at every column, pr[q][j] = T_{k+q}[r_q][j]
 // (the sweep's and the pivot-column pass's operands), and the sweep's per-row flags (blk_rflags)
-// when the block applied all P of its pivots.  One column / one row per thread, grid-stride.
-__global__ __launch_bounds__(kUpdBlock) void k_blk_prows(const double* __restrict__ T, int64_t ld,
-                                                         int rows, int m, int P,
-                                                         const BlkHdr* __restrict__ h,
-                                                         double* __restrict__ mul,
-                                                         double* __restrict__ pr) {
+// when the block applied all P of its pivots.  One column per thread (64-thread workgroups, so
+// the C columns spread over every CU), the pivot rows' values in a shift register as in
+// win_colvals, the multipliers of the pivot rows (mul[r_s][q], P x P) and the reciprocals in LDS
+// -- a global load per element update made the first form latency-bound (45.7 us per 20-pivot
+// block at 16384^2, profiles/r06d/).  The division is the hoisted-reciprocal sequence while
+// every numerator of the column stays inside the exponent window (win_term, one vote per wave),
+// else the column is recomputed with the IEEE division: the same bits either way (the fast
+// planner chains' argument, smx_block.hpp blk_chain_fd).
+constexpr int kProwsNT = kWave;
+__global__ __launch_bounds__(kProwsNT) void k_blk_prows(const double* __restrict__ T, int64_t ld,
+                                                        int rows, int m, int P,
+                                                        const BlkHdr* __restrict__ h,
+                                                        double* __restrict__ mul,
+                                                        double* __restrict__ pr) {
     __shared__ BlkPiv s_pv;
+    __shared__ double s_mp[kBlkMax][kBlkMax];   // [pivot row s][step q]: mul[r_s][q]
+    __shared__ int s_ok;
     const int peff = h->peff;
     if (peff <= 0) return;
-    blk_load_pivots(h, peff, &s_pv);
+    const int tid = threadIdx.x;
+    if (tid < peff) {
+        s_pv.r[tid] = h->r[tid];
+        s_pv.c[tid] = h->c[tid];
+        s_pv.e[tid] = h->e[tid];
+        s_pv.y[tid] = fd_prep(h->e[tid]).y;
+    }
+    if (tid == 0) s_ok = 1;
     __syncthreads();
+    if (tid < peff && !fd_prep(s_pv.e[tid]).ok) s_ok = 0;   // (ordered by the barrier below)
+    for (int t = tid; t < peff * peff; t += kProwsNT) {
+        const int sr = t / peff, q = t % peff;
+        s_mp[sr][q] = mul[(int64_t)s_pv.r[sr] * kBlkMax + q];
+    }
+    __syncthreads();
+    const bool allok = s_ok != 0;
     const int C = m + 1;
-    const int nt = (int)gridDim.x * kUpdBlock;
-    for (int j = (int)blockIdx.x * kUpdBlock + threadIdx.x; j < C; j += nt) {
-        win_colvals<0>(T, ld, j, peff, s_pv, mul, nullptr,
-                       [&](int q, double v) { pr[(int64_t)q * ld + j] = v; }, nullptr);
+    const int nt = (int)gridDim.x * kProwsNT;
+    for (int j0 = (int)blockIdx.x * kProwsNT; j0 < C; j0 += nt) {
+        const int j = min(j0 + tid, C - 1);   // (tail lanes redo the last column: no divergence)
+        double x0[kBlkMax];
+#pragma unroll
+        for (int p = 0; p < kBlkMax; ++p) x0[p] = p < peff ? T[(int64_t)s_pv.r[p] * ld + j] : 0.0;
+        for (int exact = 0; exact < 2; ++exact) {
+            double x[kBlkMax];
+#pragma unroll
+            for (int p = 0; p < kBlkMax; ++p) x[p] = x0[p];
+            uint32_t wt = 0;
+#pragma unroll 1
+            for (int q = 0; q < peff; ++q) {
+                const double p = x[0];   // T_{k+q}[r_q][j]
+                if (j0 + tid < C) pr[(int64_t)q * ld + j] = p;
+                const int rq = s_pv.r[q];
+                const bool pc = j == s_pv.c[q];
+                const double e = s_pv.e[q], y = s_pv.y[q];
+#pragma unroll
+                for (int sft = 1; sft < kBlkMax; ++sft) {
+                    const int t = q + sft;
+                    if (t < peff) {
+                        const double a = x[sft] * e;
+                        const double b = p * s_mp[t][q];
+                        const bool prow = s_pv.r[t] == rq;
+                        const double num = prow ? (pc ? 1.0 : -x[sft]) : (pc ? x[sft] : (a - b));
+                        if (exact) {
+                            x[sft] = num / e;
+                        } else {
+                            wt = max(wt, win_term(num));
+                            const double tq = num * y;
+                            const double rr = fma(-e, tq, num);
+                            x[sft] = fma(rr, y, tq);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int sft = 0; sft + 1 < kBlkMax; ++sft) x[sft] = x[sft + 1];
+            }
+            if (!exact && allok && __all(wt < kWinSpan)) break;   // every quotient exact
+        }
     }
     if (peff != P) return;
     int32_t* fl = blk_rflags(mul, rows + 1);
-    for (int i = (int)blockIdx.x * kUpdBlock + threadIdx.x; i <= rows; i += nt) {
+    for (int i = (int)blockIdx.x * kProwsNT + tid; i <= rows; i += nt) {
         const double* mr = mul + (int64_t)i * kBlkMax;
         bool bnd = true, zero = false, piv = false;
 #pragma unroll
