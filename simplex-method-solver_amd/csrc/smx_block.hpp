@@ -507,8 +507,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_start(const double* __restrict__
                                                       BlkHdr* __restrict__ h,
                                                       BlkHdr* __restrict__ h1,
                                                       double* __restrict__ fr,
-                                                      smx_part* __restrict__ parts,
-                                                      double* __restrict__ win, int nwin) {
+                                                      smx_part* __restrict__ parts) {
     __shared__ int s_tmp[kBlkNT / kWave];
     const int b = blockIdx.x, G = gridDim.x, tid = threadIdx.x;
     if (b == 0 && tid == 0) {
@@ -517,17 +516,6 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_start(const double* __restrict__
         h1->peff = 0;
     }
     if (ctl->term) return;
-    // the window planner's window of T (slot `parity`; win_fill, smx_window.hpp)
-    if (win) {
-        const int lane = tid & (kWave - 1);
-        const int jl = lane < nwin ? (m + 1 <= nwin ? (lane <= m ? lane : -1)
-                                                    : (lane < nwin - 1 ? lane : m))
-                                   : -1;
-        double* Wp = win + (int64_t)parity * (rows + 1) * kWin;
-        const int nw = G * (kBlkNT / kWave);
-        for (int i = b * (kBlkNT / kWave) + (tid >> 6); i <= rows; i += nw)
-            if (jl >= 0) Wp[(int64_t)i * kWin + lane] = T[(int64_t)i * ld + jl];
-    }
     const int C = m + 1;
     const double* f = T + (int64_t)rows * ld;
     double* fo = fr + (int64_t)parity * ld;

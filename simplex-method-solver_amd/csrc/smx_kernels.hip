@@ -570,10 +570,9 @@ BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
 // loc: buffer index (0/1) of T
 int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, smx_ctl* ctl,
                      const BlkPtrs& b, hipStream_t st) {
-    double* win = use_window(s) ? b.win : nullptr;
     hipLaunchKernelGGL(k_blk_start, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
                        fscan_of(s), parity, loc, s.row0, (const smx_ctl*)ctl, b.h[0], b.h[1],
-                       b.fr, b.parts, win, g_block_nwin);
+                       b.fr, b.parts);
     return (int)hipGetLastError();
 }
 
@@ -590,19 +589,20 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
 }
 
 // One window-planner launch (block bn, step L) and, after a block's last step, the pivot rows
+// fromT: the chain's first step (the window is read from the table itself)
 int launch_blk_wstep(int L, const double* T, const smx_shape& s, int P, int parity, int bn,
                      smx_ctl* ctl, const BlkPtrs& b, int32_t* log, double* xhist, int64_t log_cap,
-                     hipStream_t st) {
+                     hipStream_t st, int fromT) {
     hipLaunchKernelGGL(k_blk_wstep, dim3(win_groups(s.rows)), dim3(kBlkNT), 0, st, T, s.ld,
                        s.rows, s.m, s.flen, fscan_of(s), P, L, parity, bn, g_block_nwin,
-                       win_rpw(s.rows), ctl, b.h[0], b.parts, b.mul[0], b.win, log, xhist,
+                       win_rpw(s.rows), fromT, ctl, b.h[0], b.parts, b.mul[0], b.win, log, xhist,
                        log_cap);
     return (int)hipGetLastError();
 }
 int launch_blk_prows(const double* T, const smx_shape& s, int P, const BlkPtrs& b,
                      hipStream_t st) {
-    // one column per thread, 64-thread workgroups: 16384 columns over all 256 CUs
-    const int64_t work = std::max<int64_t>(s.m + 1, s.rows + 1);
+    // one column per quad of lanes (16384 columns: 1,024 waves), one row per thread for the flags
+    const int64_t work = std::max<int64_t>((int64_t)(s.m + 1) * 4, s.rows + 1);
     const int grid = (int)std::min<int64_t>((work + kProwsNT - 1) / kProwsNT, num_cus() * 8);
     hipLaunchKernelGGL(k_blk_prows, dim3(grid), dim3(kProwsNT), 0, st, T, s.ld, s.rows, s.m, P,
                        (const BlkHdr*)b.h[0], b.mul[0], b.pr[0]);
@@ -749,7 +749,8 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                 }
             }
             if (!err && !sh && use_window(s))
-                err = launch_blk_wstep(l, tin, s, Pb, p, bn, ctl, bp, log, xhist, log_cap, st);
+                err = launch_blk_wstep(l, tin, s, Pb, p, bn, ctl, bp, log, xhist, log_cap, st,
+                                       bn == 0 && l == 1);
             else if (!err)   // sharded: each rank writes the x-history of the label rows it owns
                 err = launch_blk_step(sh, l, tin, s, Pb, p, bn, ctl, bp, recv, nranks, log,
                                       xhist, log_cap, st, xrow,

@@ -132,7 +132,8 @@ __device__ __forceinline__ double win_chain(const double* __restrict__ T, int64_
 // constraint rows [w rpw, (w + 1) rpw).  W = the window, [2][rows + 1][kWin] by step parity.
 __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int P, int L,
-    int parity, int bn, int nwin, int rpw, smx_ctl* __restrict__ ctl, BlkHdr* __restrict__ h,
+    int parity, int bn, int nwin, int rpw, int fromT, smx_ctl* __restrict__ ctl,
+    BlkHdr* __restrict__ h,
     smx_part* __restrict__ parts, double* __restrict__ mul, double* __restrict__ W,
     int32_t* __restrict__ log, double* __restrict__ xhist, int64_t log_cap) {
     __shared__ BlkPiv s_pv;
@@ -148,32 +149,66 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     const int C = m + 1;
     const int64_t WR = (int64_t)rows + 1;
     const int jl = win_col(lane, nwin, C);   // this lane's column
-    const double* __restrict__ Wo = W + (int64_t)sp * WR * kWin;   // T_{k+D} at the window
     double* __restrict__ Wn = W + (int64_t)(sp ^ 1) * WR * kWin;   // T_{k+L}
+    // T_{k+D} at the window: the window of the step before, or at a chain's first step the table
+    // itself at the window's columns (no fill pass)
+    const double* __restrict__ So = fromT ? T : W + (int64_t)sp * WR * kWin;
+    const int64_t sld = fromT ? ld : kWin;
+    const int sj = fromT ? jl : lane;
+    auto wold = [&](int i) -> double { return jl >= 0 ? So[(int64_t)i * sld + sj] : 0.0; };
     // Everything that does not depend on the decision is loaded with the decision's operands
     // (one round trip): the stop flag, the pivots so far, the f-row's window, this wave's first
-    // rows.  On a stopped chain those loads read stale scratch and are discarded.
+    // rows.  The records go first: a wave's loads return in order, and behind the window rows
+    // (8 MB over the chip at 16384 rows) the decision waited ~2 us longer (profiles/r06f/).  On
+    // a stopped chain those loads read stale scratch and are discarded.
     SMX_BLK_STAMP(0);
     const int stopped = ctl->term;
+    constexpr int RU = kBlkPartsMax / kWave;
+    smx_part rp[RU];
+    int cD = SMX_NONE;
+    if (wid == 0) {
+        cD = h->cfs[blk_slot(D, P, bn)];
+        const smx_part* __restrict__ slot = parts + (int64_t)blk_slot(D, P, bn) * G;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            const int k = lane + u * kWave;
+            rp[u] = k < G ? slot[k] : smx_part{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
+        }
+    }
+    asm volatile("" ::: "memory");   // (issue order only: nothing waits here)
     blk_load_pivots(h, D, &s_pv);
-    const double fo = jl >= 0 ? Wo[(int64_t)rows * kWin + lane] : 0.0;
+    const double fo = wold(rows);
     const int i0 = (b * (kBlkNT / kWave) + wid) * rpw;
     const int i1 = min(rows, i0 + rpw);
     // this wave's first two batches of rows (the row pass keeps two batches in flight)
     double xv[kWinBatch], xn[kWinBatch];
 #pragma unroll
     for (int u = 0; u < kWinBatch; ++u) {
-        xv[u] = (i0 + u < i1 && jl >= 0) ? Wo[(int64_t)(i0 + u) * kWin + lane] : 0.0;
-        xn[u] = (i0 + kWinBatch + u < i1 && jl >= 0)
-                    ? Wo[(int64_t)(i0 + kWinBatch + u) * kWin + lane] : 0.0;
+        xv[u] = i0 + u < i1 ? wold(i0 + u) : 0.0;
+        xn[u] = i0 + kWinBatch + u < i1 ? wold(i0 + kWinBatch + u) : 0.0;
     }
     if (wid == 0) {
-        // the decision of step D from its records (every workgroup, identically)
-        const int c = h->cfs[blk_slot(D, P, bn)];
+        // the decision of step D from its records (every workgroup, identically; the order of
+        // the merges is immaterial: total orders)
+        const int c = cD;
         int nb;
         First f;
         Cand bb;
-        blk_merge_records(parts + (int64_t)blk_slot(D, P, bn) * G, G, nb, f, bb);
+        {
+            int n0 = SMX_NONE;
+            First fi{SMX_NONE, 0.0};
+            Cand bq = cand_none();
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                n0 = min(n0, rp[u].p1col);
+                if (rp[u].first < fi.idx) fi = First{rp[u].first, rp[u].first_v};
+                const Cand o{rp[u].best_cls, rp[u].best_i, rp[u].best_v};
+                if (better(o, bq)) bq = o;
+            }
+            nb = wave_min_int_dpp(n0);
+            f = wave_first_dpp(fi);
+            bb = wave_best_dpp(bq);
+        }
         Decision d;
         d.c = c;
         d.r = SMX_NONE;
@@ -224,7 +259,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         return;
     }
     const int r = d.r;
-    const double pw = jl >= 0 ? Wo[(int64_t)r * kWin + lane] : 0.0;   // T_{k+D}[r][jl]
+    const double pw = wold(r);   // T_{k+D}[r][jl]
     int c = d.c;
     if (nb != SMX_NONE) {
         // phase 1: first j < m with T_{k+D}[r][j] > 0 (simplex.py:81-85); the lanes hold the
@@ -351,6 +386,9 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     // another, the pass took 9.2 us of a 15.3 us step at 16 rows per wave, profiles/r06e/.)
     const int ms = __builtin_amdgcn_readfirstlane(win_slot(m, nwin, C));
     double* __restrict__ mT = blk_mulT(mul, rows + 1);
+    const FastDiv efd = fd_prep(e);
+    const double ey = efd.y;
+    const bool eok = efd.ok;
     BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
     for (int ib = i0; ib < i1; ib += kWinBatch) {
         // fallbacks (columns outside the window): lane u derives row ib + u's value from T_k
@@ -362,8 +400,26 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         double mc[kWinBatch], nv[kWinBatch];
 #pragma unroll
         for (int u = 0; u < kWinBatch; ++u) mc[u] = __shfl(cs >= 0 ? xv[u] : mcv, cs >= 0 ? cs : u);
+        // the hoisted-reciprocal division while every numerator of the batch lies inside the
+        // exponent window (win_term; the planner chains' argument, smx_block.hpp blk_chain_fd),
+        // else the batch again with the IEEE division: the same bits either way
+        uint32_t wt = 0;
 #pragma unroll
-        for (int u = 0; u < kWinBatch; ++u) nv[u] = win_upd(xv[u], ib + u == r, jl == c, pw, mc[u], e);
+        for (int u = 0; u < kWinBatch; ++u) {
+            const double a = xv[u] * e;
+            const double bq = pw * mc[u];
+            const bool pc = jl == c;
+            const double num = (ib + u == r) ? (pc ? 1.0 : -xv[u]) : (pc ? xv[u] : (a - bq));
+            wt = max(wt, win_term(num));
+            const double tq = num * ey;
+            const double rr = fma(-e, tq, num);
+            nv[u] = fma(rr, ey, tq);
+        }
+        if (!eok || !__all(jl < 0 || wt < kWinSpan)) {
+#pragma unroll
+            for (int u = 0; u < kWinBatch; ++u)
+                nv[u] = win_upd(xv[u], ib + u == r, jl == c, pw, mc[u], e);
+        }
 #pragma unroll
         for (int u = 0; u < kWinBatch; ++u)
             if (ib + u < i1 && jl >= 0) Wn[(int64_t)(ib + u) * kWin + lane] = nv[u];
@@ -372,7 +428,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         for (int u = 0; u < kWinBatch; ++u) {
             xv[u] = xn[u];
             const int i2 = ib + 2 * kWinBatch + u;
-            if (i2 < i1 && jl >= 0) xn[u] = Wo[(int64_t)i2 * kWin + lane];
+            if (i2 < i1) xn[u] = wold(i2);
         }
         double myc = 0.0, mybv = 0.0, mya = 0.0;
 #pragma unroll
@@ -405,15 +461,17 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
 
 // After a block's last planner step: the pivot rows at every column, pr[q][j] = T_{k+q}[r_q][j]
 // (the sweep's and the pivot-column pass's operands), and the sweep's per-row flags (blk_rflags)
-// when the block applied all P of its pivots.  One column per thread (64-thread workgroups, so
-// the C columns spread over every CU), the pivot rows' values in a shift register as in
-// win_colvals, the multipliers of the pivot rows (mul[r_s][q], P x P) and the reciprocals in LDS
-// -- a global load per element update made the first form latency-bound (45.7 us per 20-pivot
-// block at 16384^2, profiles/r06d/).  The division is the hoisted-reciprocal sequence while
-// every numerator of the column stays inside the exponent window (win_term, one vote per wave),
-// else the column is recomputed with the IEEE division: the same bits either way (the fast
-// planner chains' argument, smx_block.hpp blk_chain_fd).
-constexpr int kProwsNT = kWave;
+// when the block applied all P of its pivots.  Every column is one quad of lanes: lane k of the
+// quad holds the pivot rows s = 4u + k (u < kQ) of that column; step q takes pivot row q's value
+// from its lane (ds_bpermute) and every lane applies pivot q to its later pivot rows, with the
+// pivot rows' multipliers (mul[r_s][q]) and the reciprocals in LDS.  (One column per thread with a
+// global load per element update took 45.7 us per 20-pivot block at 16384^2, with the
+// multipliers in LDS 34.7 us, profiles/r06d/, r06f/: one wave per SIMD on a quarter of the chip,
+// each lane a 190-step triangle.)  The division is the hoisted-reciprocal sequence while every
+// numerator of the wave stays inside the exponent window (win_term, one vote), else the columns
+// again with the IEEE division: the same bits either way (smx_block.hpp blk_chain_fd).
+constexpr int kProwsNT = kUpdBlock;
+constexpr int kProwsQ = kBlkMax / 4;   // pivot rows per lane
 __global__ __launch_bounds__(kProwsNT) void k_blk_prows(const double* __restrict__ T, int64_t ld,
                                                         int rows, int m, int P,
                                                         const BlkHdr* __restrict__ h,
@@ -424,7 +482,7 @@ __global__ __launch_bounds__(kProwsNT) void k_blk_prows(const double* __restrict
     __shared__ int s_ok;
     const int peff = h->peff;
     if (peff <= 0) return;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1);
     if (tid < peff) {
         s_pv.r[tid] = h->r[tid];
         s_pv.c[tid] = h->c[tid];
@@ -441,50 +499,61 @@ __global__ __launch_bounds__(kProwsNT) void k_blk_prows(const double* __restrict
     __syncthreads();
     const bool allok = s_ok != 0;
     const int C = m + 1;
-    const int nt = (int)gridDim.x * kProwsNT;
-    for (int j0 = (int)blockIdx.x * kProwsNT; j0 < C; j0 += nt) {
-        const int j = min(j0 + tid, C - 1);   // (tail lanes redo the last column: no divergence)
-        double x0[kBlkMax];
+    const int k = lane & 3;              // this lane's pivot rows: s = 4 u + k
+    const int qbase = lane & ~3;         // the quad's first lane
+    const int64_t ncol = (int64_t)gridDim.x * (kProwsNT / 4);
+    for (int64_t j0 = (int64_t)blockIdx.x * (kProwsNT / 4); j0 < C; j0 += ncol) {
+        const int jq = (int)j0 + (tid >> 2);
+        const int j = jq < C ? jq : C - 1;   // (tail quads redo the last column)
+        double x0[kProwsQ];
 #pragma unroll
-        for (int p = 0; p < kBlkMax; ++p) x0[p] = p < peff ? T[(int64_t)s_pv.r[p] * ld + j] : 0.0;
+        for (int u = 0; u < kProwsQ; ++u) {
+            const int sr = 4 * u + k;
+            x0[u] = sr < peff ? T[(int64_t)s_pv.r[sr] * ld + j] : 0.0;
+        }
         for (int exact = 0; exact < 2; ++exact) {
-            double x[kBlkMax];
+            double x[kProwsQ];
 #pragma unroll
-            for (int p = 0; p < kBlkMax; ++p) x[p] = x0[p];
+            for (int u = 0; u < kProwsQ; ++u) x[u] = x0[u];
             uint32_t wt = 0;
 #pragma unroll 1
             for (int q = 0; q < peff; ++q) {
-                const double p = x[0];   // T_{k+q}[r_q][j]
-                if (j0 + tid < C) pr[(int64_t)q * ld + j] = p;
+                // T_{k+q}[r_q][j]: slot q / 4 of quad lane q % 4 (updated by the q pivots before)
+                const int uq = q >> 2;
+                double mine = x[0];
+#pragma unroll
+                for (int u = 1; u < kProwsQ; ++u)
+                    if (u == uq) mine = x[u];
+                const double p = __shfl(mine, qbase | (q & 3));
+                if (k == 0 && jq < C) pr[(int64_t)q * ld + j] = p;
                 const int rq = s_pv.r[q];
                 const bool pc = j == s_pv.c[q];
                 const double e = s_pv.e[q], y = s_pv.y[q];
 #pragma unroll
-                for (int sft = 1; sft < kBlkMax; ++sft) {
-                    const int t = q + sft;
-                    if (t < peff) {
-                        const double a = x[sft] * e;
-                        const double b = p * s_mp[t][q];
-                        const bool prow = s_pv.r[t] == rq;
-                        const double num = prow ? (pc ? 1.0 : -x[sft]) : (pc ? x[sft] : (a - b));
+                for (int u = 0; u < kProwsQ; ++u) {
+                    const int sr = 4 * u + k;
+                    if (sr > q && sr < peff) {
+                        const double a = x[u] * e;
+                        const double b = p * s_mp[sr][q];
+                        const bool prow = s_pv.r[sr] == rq;
+                        const double num = prow ? (pc ? 1.0 : -x[u]) : (pc ? x[u] : (a - b));
                         if (exact) {
-                            x[sft] = num / e;
+                            x[u] = num / e;
                         } else {
                             wt = max(wt, win_term(num));
                             const double tq = num * y;
                             const double rr = fma(-e, tq, num);
-                            x[sft] = fma(rr, y, tq);
+                            x[u] = fma(rr, y, tq);
                         }
                     }
                 }
-#pragma unroll
-                for (int sft = 0; sft + 1 < kBlkMax; ++sft) x[sft] = x[sft + 1];
             }
             if (!exact && allok && __all(wt < kWinSpan)) break;   // every quotient exact
         }
     }
     if (peff != P) return;
     int32_t* fl = blk_rflags(mul, rows + 1);
+    const int nt = (int)gridDim.x * kProwsNT;
     for (int i = (int)blockIdx.x * kProwsNT + tid; i <= rows; i += nt) {
         const double* mr = mul + (int64_t)i * kBlkMax;
         bool bnd = true, zero = false, piv = false;
