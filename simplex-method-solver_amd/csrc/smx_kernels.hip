@@ -593,7 +593,7 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
 int launch_blk_wstep(int L, const double* T, const smx_shape& s, int P, int parity, int bn,
                      smx_ctl* ctl, const BlkPtrs& b, int32_t* log, double* xhist, int64_t log_cap,
                      hipStream_t st, int fromT) {
-    hipLaunchKernelGGL(k_blk_wstep, dim3(win_groups(s.rows)), dim3(kBlkNT), 0, st, T, s.ld,
+    hipLaunchKernelGGL(k_blk_wstep, dim3(win_groups(s.rows)), dim3(kWinNT), 0, st, T, s.ld,
                        s.rows, s.m, s.flen, fscan_of(s), P, L, parity, bn, g_block_nwin,
                        win_rpw(s.rows), fromT, ctl, b.h[0], b.parts, b.mul[0], b.win, log, xhist,
                        log_cap);

@@ -32,18 +32,23 @@ namespace {
 // both planners, and with windows of 2..64 columns to drive the fallbacks).
 // (kWin = 64 window slots per row, one wave's lanes: smx_block.hpp, beside the scratch layout)
 constexpr int kWinMaxG = 256;     // planner workgroups at most (the records merge: kBlkPartsMax)
+// Eight waves per workgroup: 2,048 waves at 16384 rows, eight rows each (one batch), two per
+// SIMD.  (Four waves of 16 rows: the row pass, a dependent chain of shuffles, divisions and
+// stores per batch on one wave per SIMD, took 4.2 us of a 12 us step, profiles/r06g/.)
+constexpr int kWinNT = 512;
+constexpr int kWinWaves = kWinNT / kWave;
 constexpr int kWinBatch = 8;      // rows of a wave updated together (two batches in flight)
 static_assert(kWinMaxG <= kBlkPartsMax, "window planner records");
 
 // Rows per wave and workgroups of a window step for `rows` constraint rows: four waves per
 // workgroup, at most kWinMaxG workgroups (16384 rows: 16 per wave on 256 workgroups)
 __host__ __device__ __forceinline__ int win_rpw(int rows) {
-    const int w = kWinMaxG * (kBlkNT / kWave);
+    const int w = kWinMaxG * kWinWaves;
     const int r = (rows + w - 1) / w;
     return r < 1 ? 1 : r;
 }
 __host__ __device__ __forceinline__ int win_groups(int rows) {
-    const int per = win_rpw(rows) * (kBlkNT / kWave);
+    const int per = win_rpw(rows) * kWinWaves;
     const int g = (rows + per - 1) / per;
     return g < 1 ? 1 : g;
 }
@@ -128,9 +133,9 @@ __device__ __forceinline__ double win_chain(const double* __restrict__ T, int64_
 }
 
 // One pivot of the block (step L: decide block step D = L - 1, apply it to the window, build the
-// records of step L).  Grid: win_groups(rows) workgroups of kBlkNT threads; wave w owns
+// records of step L).  Grid: win_groups(rows) workgroups of kWinNT threads; wave w owns
 // constraint rows [w rpw, (w + 1) rpw).  W = the window, [2][rows + 1][kWin] by step parity.
-__global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
+__global__ __launch_bounds__(kWinNT) void k_blk_wstep(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int P, int L,
     int parity, int bn, int nwin, int rpw, int fromT, smx_ctl* __restrict__ ctl,
     BlkHdr* __restrict__ h,
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     __shared__ int s_nb, s_cfD;
     __shared__ double s_e, s_fc, s_prcf;
     __shared__ double s_colc[kBlkMax], s_colf[kBlkMax];   // pivot rows at c / cf (fallbacks)
-    __shared__ int s_tmp[kBlkNT / kWave];
+    __shared__ int s_tmp[kWinWaves];
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
     const int b = blockIdx.x, G = gridDim.x;
     const int D = L - 1;
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
     asm volatile("" ::: "memory");   // (issue order only: nothing waits here)
     blk_load_pivots(h, D, &s_pv);
     const double fo = wold(rows);
-    const int i0 = (b * (kBlkNT / kWave) + wid) * rpw;
+    const int i0 = (b * kWinWaves + wid) * rpw;
     const int i1 = min(rows, i0 + rpw);
     // this wave's first two batches of rows (the row pass keeps two batches in flight)
     double xv[kWinBatch], xn[kWinBatch];
@@ -235,7 +240,9 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
             s_cfD = c;
         }
     }
-    __syncthreads();
+    // A barrier for the LDS hand-off only: __syncthreads() would first wait for every wave's
+    // outstanding loads -- the whole row prefetch (profiles/r06g/: the decision at ~4.5 us)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     SMX_BLK_STAMP(1);
     if (stopped) {
         if (D == 0 && b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         if (p1 == SMX_NONE && C > nwin) {
             // the columns past the window, T_{k+D}[r][j] from T_k (rounds with early exit; the
             // same minimum in every workgroup)
-            for (int j0 = nwin - 1; j0 < m && p1 == SMX_NONE; j0 += kBlkNT) {
+            for (int j0 = nwin - 1; j0 < m && p1 == SMX_NONE; j0 += kWinNT) {
                 const int j = j0 + tid;
                 int mine = SMX_NONE;
                 if (j < m) {
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
                     win_colvals<1>(T, ld, j, D, s_pv, mul, xr, [](int, double) {}, xo);
                     if (xo[0] > 0.0) mine = j;
                 }
-                p1 = block_min_int_dpp<kBlkNT>(mine, s_tmp);
+                p1 = block_min_int_dpp<kWinNT>(mine, s_tmp);
             }
         }
         if (p1 == SMX_NONE) {
@@ -317,7 +324,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         const unsigned long long bal = __ballot(jl >= 0 && jl < fscan && fn < 0.0);
         cf = bal ? win_col(__ffsll((long long)bal) - 1, nwin, C) : SMX_NONE;
         if (cf == SMX_NONE && C > nwin) {
-            for (int j0 = nwin - 1; j0 < fscan && cf == SMX_NONE; j0 += kBlkNT) {
+            for (int j0 = nwin - 1; j0 < fscan && cf == SMX_NONE; j0 += kWinNT) {
                 const int j = j0 + tid;
                 int mine = SMX_NONE;
                 if (j < fscan) {
@@ -326,7 +333,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
                     win_colvals<2>(T, ld, j, D, s_pv, mul, xr, [](int, double) {}, xo);
                     if (win_upd(xo[1], false, j == c, xo[0], fc, e) < 0.0) mine = j;
                 }
-                cf = block_min_int_dpp<kBlkNT>(mine, s_tmp);
+                cf = block_min_int_dpp<kWinNT>(mine, s_tmp);
             }
         }
     }
@@ -455,7 +462,31 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_wstep(
         }
     }
     SMX_BLK_STAMP(5);
-    blk_rec_store(R, parts + (int64_t)blk_slot(L, P, bn) * G + b);   // DPP per wave, then the 4 waves
+    {
+        // the workgroup's record: DPP per wave, then wave 0 merges the eight (total orders)
+        __shared__ BlkRec s_r[kWinWaves];
+        const int n0 = wave_min_int_dpp(R.nb);
+        const First f0 = wave_first_dpp(R.f);
+        const Cand c0 = wave_best_dpp(R.bc);
+        if (lane == 0) s_r[wid] = BlkRec{n0, f0, c0};
+        __syncthreads();
+        if (tid == 0) {
+            BlkRec a = s_r[0];
+            for (int w = 1; w < kWinWaves; ++w) {
+                a.nb = min(a.nb, s_r[w].nb);
+                if (s_r[w].f.idx < a.f.idx) a.f = s_r[w].f;
+                if (better(s_r[w].bc, a.bc)) a.bc = s_r[w].bc;
+            }
+            smx_part pt;
+            pt.p1col = a.nb;
+            pt.first = a.f.idx;
+            pt.first_v = a.f.v;
+            pt.best_cls = a.bc.cls;
+            pt.best_i = a.bc.idx;
+            pt.best_v = a.bc.v;
+            parts[(int64_t)blk_slot(L, P, bn) * G + b] = pt;
+        }
+    }
     SMX_BLK_STAMP(7);
 }
 
