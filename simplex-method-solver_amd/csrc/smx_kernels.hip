@@ -626,9 +626,15 @@ int launch_bsh_pick(const double* hdrs, const smx_shape& s, int nranks, int rank
     return (int)hipGetLastError();
 }
 
+// The pack's grid: the records are merged by count (blk_parts_of, the step kernels' partition),
+// while the grid only slices the candidate rows' columns -- one column per thread (a rank of
+// 2,049 rows had ~9 workgroups, so every thread carried ~8 columns' chains of up to P - 1 steps
+// one after the other: most of the sharded per-pivot floor)
 int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
                     const smx_ctl* ctl, const BlkPtrs& b, double* send, hipStream_t st) {
-    hipLaunchKernelGGL(bsh_pack_fn(D), dim3(blk_parts_of(s.nparts, s.rows)), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
+    const int gc = (int)std::min<int64_t>((s.m + 1 + kBlkNT - 1) / kBlkNT, kBlkPartsMax);
+    const int grid = std::max(blk_parts_of(s.nparts, s.rows), gc);
+    hipLaunchKernelGGL(bsh_pack_fn(D), dim3(grid), dim3(kBlkNT), 0, st, T, s.ld, s.rows,
                        s.m, s.row0, P, bn, ctl, (const BlkHdr*)b.h[0], (const smx_part*)b.parts,
                        blk_parts_of(s.nparts, s.rows), (const double*)b.mul[0], (const double*)b.pr[0], send);
     return (int)hipGetLastError();

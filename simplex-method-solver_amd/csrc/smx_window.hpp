@@ -159,8 +159,14 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wstep(
     // itself at the window's columns (no fill pass)
     const double* __restrict__ So = fromT ? T : W + (int64_t)sp * WR * kWin;
     const int64_t sld = fromT ? ld : kWin;
-    const int sj = fromT ? jl : lane;
-    auto wold = [&](int i) -> double { return jl >= 0 ? So[(int64_t)i * sld + sj] : 0.0; };
+    const int sj = fromT ? max(jl, 0) : lane;
+    // Every load of the prologue is unconditional (rows and columns clamped, results masked): a
+    // load behind a branch leaves the compiler unable to count the loads in flight, and it then
+    // waits for all of them -- the decision behind the whole row prefetch (profiles/r06h/).
+    auto wold = [&](int i) -> double {
+        const double v = So[(int64_t)i * sld + sj];
+        return jl >= 0 ? v : 0.0;
+    };
     // Everything that does not depend on the decision is loaded with the decision's operands
     // (one round trip): the stop flag, the pivots so far, the f-row's window, this wave's first
     // rows.  The records go first: a wave's loads return in order, and behind the window rows
@@ -175,10 +181,10 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wstep(
         cD = h->cfs[blk_slot(D, P, bn)];
         const smx_part* __restrict__ slot = parts + (int64_t)blk_slot(D, P, bn) * G;
 #pragma unroll
-        for (int u = 0; u < RU; ++u) {
-            const int k = lane + u * kWave;
-            rp[u] = k < G ? slot[k] : smx_part{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
-        }
+        for (int u = 0; u < RU; ++u) rp[u] = slot[min(lane + u * kWave, G - 1)];
+#pragma unroll
+        for (int u = 0; u < RU; ++u)
+            if (lane + u * kWave >= G) rp[u] = smx_part{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
     }
     asm volatile("" ::: "memory");   // (issue order only: nothing waits here)
     blk_load_pivots(h, D, &s_pv);
@@ -189,8 +195,8 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wstep(
     double xv[kWinBatch], xn[kWinBatch];
 #pragma unroll
     for (int u = 0; u < kWinBatch; ++u) {
-        xv[u] = i0 + u < i1 ? wold(i0 + u) : 0.0;
-        xn[u] = i0 + kWinBatch + u < i1 ? wold(i0 + kWinBatch + u) : 0.0;
+        xv[u] = wold(i0 + u < i1 ? i0 + u : rows);
+        xn[u] = wold(i0 + kWinBatch + u < i1 ? i0 + kWinBatch + u : rows);
     }
     if (wid == 0) {
         // the decision of step D from its records (every workgroup, identically; the order of
@@ -435,7 +441,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wstep(
         for (int u = 0; u < kWinBatch; ++u) {
             xv[u] = xn[u];
             const int i2 = ib + 2 * kWinBatch + u;
-            if (i2 < i1) xn[u] = wold(i2);
+            xn[u] = wold(i2 < i1 ? i2 : rows);
         }
         double myc = 0.0, mybv = 0.0, mya = 0.0;
 #pragma unroll
@@ -469,7 +475,9 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wstep(
         const First f0 = wave_first_dpp(R.f);
         const Cand c0 = wave_best_dpp(R.bc);
         if (lane == 0) s_r[wid] = BlkRec{n0, f0, c0};
-        __syncthreads();
+        // LDS only: the row pass's stores need not land before the record goes out (the kernel's
+        // end waits for them anyway)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (tid == 0) {
             BlkRec a = s_r[0];
             for (int w = 1; w < kWinWaves; ++w) {

@@ -17,6 +17,8 @@
 #                          GRBM_COUNT SQ_INSTS_VALU SQ_BUSY_CYCLES of bench200 (the clock per sweep)
 #   clock20                the same counters over the driver's bench20 line (the timed sweep's clock)
 #   paths=ARGS             tools/sweep_paths.py ARGS on the diagnostic build (libsmx_diag.so)
+#   pmcpaths=ARGS          rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY
+#                          GRBM_GUI_ACTIVE of tools/sweep_paths.py ARGS (product build; per sweep)
 #   sweeps=ARGS            tools/sweep_paths.py ARGS on the product build (timings only)
 #   sweepslib=LIB,ARGS     tools/sweep_paths.py ARGS on another build of libsmx (SMX_LIB=LIB: an A/B)
 #   blockbench=ARGS        tools/block_bench.py ARGS
@@ -64,6 +66,7 @@ for spec in "$@"; do
     sq20) cmd="cd /tmp && timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -d $O/sq20 -o run --output-format csv -- $B --steps 20 --warmup 5"; d=300 ;;
     clock20) cmd="cd /tmp && timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VALU SQ_BUSY_CYCLES -d $O/clock20 -o run --output-format csv -- $B --steps 20 --warmup 5 --sustained 0"; d=300 ;;
     clock200) cmd="cd /tmp && timeout -s KILL 240 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VALU SQ_BUSY_CYCLES -d $O/clock200 -o run --output-format csv -- $B --steps 200 --warmup 20"; d=300 ;;
+    pmcpaths) cmd="cd /tmp && timeout -s KILL 280 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d $O/$tag -o run --output-format csv -- python3 $R/tools/sweep_paths.py $arg"; d=300 ;;
     paths) cmd="cd $R && SMX_LIB=libsmx_diag.so python -u tools/sweep_paths.py $arg"; d=300 ;;
     sweeps) cmd="cd $R && python -u tools/sweep_paths.py $arg"; d=300 ;;
     sweepslib) lib="${arg%% *}"; cmd="cd $R && SMX_LIB=$lib python -u tools/sweep_paths.py ${arg#* }"; d=300 ;;
