@@ -1484,7 +1484,15 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
             }
             ok = true;
         } else if (allok && rf != 2) {   // not a pivot row (rf == 2): the window-tracked path
-            // numerators checked once per row by a vote
+            // numerators checked once per row by a vote.  Exact zeros are inside the domain too
+            // (round 6): fd_zero's v_div_fixup gives a zero numerator its sign, every other
+            // numerator must lie in the exponent window (a finite nonzero one in it, a normal
+            // quotient: div_fixup returns the hoisted sequence's quotient unchanged).  A pivot
+            // column's lane computes RN(x e) - RN(e x) = +0 at its step like on the fast path and
+            // is rewritten by blk_fixcols.  (Counting zeros as outside sent every unit of a chunk
+            // with a pivot-row value outside the bounds to the exact path on config 5's integer
+            // tables -- a few chunks' waves 5-10x slower than the rest, block 0 at 2x block 2's
+            // time with ~1.2x its instructions: profiles/r06i/7_paths.log, 8_pmcpaths/.)
             uint32_t wt = 0;
 #pragma unroll
             for (int q = 0; q < P; ++q) {
@@ -1497,10 +1505,9 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                 double rr[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
-                    wt = max(wt, win_term(n[k]));
-                    const double tq = n[k] * y;
-                    const double r = fma(-e, tq, n[k]);
-                    rr[k] = fma(r, y, tq);
+                    const uint32_t tk = win_term(n[k]);
+                    wt = max(wt, (dbits(n[k]) << 1) == 0 ? 0u : tk);
+                    rr[k] = fd_zero(n[k], e, y);
                 }
                 v0 = dbl2{rr[0], rr[1]};
             }

@@ -545,12 +545,16 @@ struct BlkPtrs {
 // it to drive the window's fallbacks).
 int g_block_planner = 0;
 int g_block_nwin = kWin;
-bool use_window(const smx_shape& s) { return g_block_planner == 0 && s.row0 == 0 && s.rows == s.n; }
+// (sh: a row-sharded chain -- at world size 1 its shape is the whole table, so the shape alone
+// cannot tell)
+bool use_window(const smx_shape& s, bool sh) {
+    return !sh && g_block_planner == 0 && s.row0 == 0 && s.rows == s.n;
+}
 
 // Planner workgroups of a chain (every launch of one chain uses the same count, since a step
 // merges the records of the step before it by that count)
-int blk_G(const smx_shape& s) {
-    return use_window(s) ? win_groups(s.rows) : blk_parts_of(s.nparts, s.rows);
+int blk_G(const smx_shape& s, bool sh) {
+    return use_window(s, sh) ? win_groups(s.rows) : blk_parts_of(s.nparts, s.rows);
 }
 
 BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
@@ -568,9 +572,9 @@ BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
 }
 
 // loc: buffer index (0/1) of T
-int launch_blk_prime(const double* T, const smx_shape& s, int parity, int loc, smx_ctl* ctl,
+int launch_blk_prime(bool sh, const double* T, const smx_shape& s, int parity, int loc, smx_ctl* ctl,
                      const BlkPtrs& b, hipStream_t st) {
-    hipLaunchKernelGGL(k_blk_start, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
+    hipLaunchKernelGGL(k_blk_start, dim3(blk_G(s, sh)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
                        fscan_of(s), parity, loc, s.row0, (const smx_ctl*)ctl, b.h[0], b.h[1],
                        b.fr, b.parts);
     return (int)hipGetLastError();
@@ -582,7 +586,7 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
                     int32_t* log, double* xhist, int64_t log_cap, hipStream_t st,
                     const double* xrow = nullptr, int64_t xslot = 0) {
     BlkStepFn fn = sh ? blk_step_fn_sh<true>(L) : blk_step_fn_sh<false>(L);
-    hipLaunchKernelGGL(fn, dim3(blk_G(s)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
+    hipLaunchKernelGGL(fn, dim3(blk_G(s, sh)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m, s.flen,
                        fscan_of(s), s.row0, P, parity, bn, ctl, b.h[0], b.parts, b.mul[0],
                        b.pr[0], b.fr, recv, nranks, log, xhist, log_cap, xrow, xslot);
     return (int)hipGetLastError();
@@ -640,10 +644,10 @@ int launch_bsh_pack(int D, const double* T, const smx_shape& s, int P, int bn,
     return (int)hipGetLastError();
 }
 
-int launch_blk_publish(const smx_shape& s, int parity, int bn, smx_ctl* ctl, const BlkPtrs& b,
+int launch_blk_publish(bool sh, const smx_shape& s, int parity, int bn, smx_ctl* ctl, const BlkPtrs& b,
                        hipStream_t st) {
     hipLaunchKernelGGL(k_blk_publish, dim3(1), dim3(kWave), 0, st, (const BlkHdr*)b.h[0],
-                       (const smx_part*)b.parts, blk_G(s), blk_slot(0, 1, bn), parity, ctl);
+                       (const smx_part*)b.parts, blk_G(s, sh), blk_slot(0, 1, bn), parity, ctl);
     return (int)hipGetLastError();
 }
 
@@ -668,7 +672,7 @@ int sweep_grid_lds(const smx_shape& s, int bpc) {
 // unpipelined chains; -1: never in place); plan slot `slot`.  pub_ctl (the chain's last block):
 // the pivot-column pass also publishes the chain's final state (block pub_bn's first records,
 // parity pub_parity) -- k_blk_publish's work without its launch.
-int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, char* blk,
+int launch_block_sweep(bool sh, double* tin, double* tother, const smx_shape& s, int P, char* blk,
                        const BlkLayout& L, hipStream_t st, int slot = 0, int ipx = 0,
                        int in_idx = 0, int ipx_part = 0, smx_ctl* pub_ctl = nullptr,
                        int pub_bn = 0, int pub_parity = 0) {
@@ -706,7 +710,7 @@ int launch_block_sweep(double* tin, double* tother, const smx_shape& s, int P, c
                                                  std::min<int64_t>(fix_wg, num_cus() * 8));
     hipLaunchKernelGGL(k_blk_sweep_rest, dim3(rest_grid), dim3(kUpdBlock), 0, st, tin,
                        tother, s.ld, s.rows + 1, s.m + 1, P, h, mul, pr, hs, ipx_part, in_idx, 1,
-                       ipx, reinterpret_cast<const smx_part*>(blk + L.parts), blk_G(s),
+                       ipx, reinterpret_cast<const smx_part*>(blk + L.parts), blk_G(s, sh),
                        blk_slot(0, 1, pub_bn), pub_parity, pub_ctl);
     return (int)hipGetLastError();
 }
@@ -728,7 +732,7 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
     int rank = 0;
     if (light && ncclCommUserRank(comm, &rank) != ncclSuccess) return (int)hipErrorInvalidValue;
     double* xrow = light ? recv + (size_t)nranks * SMX_SHARD_HDR : nullptr;
-    int err = launch_blk_prime(parity ? buf1 : buf0, s, parity, parity, ctl, bp, st);
+    int err = launch_blk_prime(sh, parity ? buf1 : buf0, s, parity, parity, ctl, bp, st);
     int p = parity, done = 0, bn = 0;
     while (!err && done < k) {
         // blocks of near-equal size (every rank of a sharded chain cuts k the same way; the
@@ -754,7 +758,7 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                     if (r != ncclSuccess) err = -1000 - (int)r;
                 }
             }
-            if (!err && !sh && use_window(s))
+            if (!err && use_window(s, sh))
                 err = launch_blk_wstep(l, tin, s, Pb, p, bn, ctl, bp, log, xhist, log_cap, st,
                                        bn == 0 && l == 1);
             else if (!err)   // sharded: each rank writes the x-history of the label rows it owns
@@ -769,11 +773,11 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                                       xhist, log_cap, st, xrow, 0);
 #endif
         }
-        if (!err && !sh && use_window(s)) err = launch_blk_prows(tin, s, Pb, bp, st);
+        if (!err && use_window(s, sh)) err = launch_blk_prows(tin, s, Pb, bp, st);
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
         const bool lastb = done + Pb >= k;   // its pivot-column pass publishes the chain
         if (!err)
-            err = launch_block_sweep(tin, toth, s, Pb, blk, bp.L, st, 0, 0, p, 0,
+            err = launch_block_sweep(sh, tin, toth, s, Pb, blk, bp.L, st, 0, 0, p, 0,
                                      lastb ? ctl : nullptr, bn + 1, (p + Pb) & 1);
         if (ev) (void)hipEventRecord(ev[2 * bn + 1], st);
         p = (p + Pb) & 1;
@@ -781,7 +785,7 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
         ++bn;
     }
     if (err) return err;
-    return bn == 0 ? launch_blk_publish(s, p, bn, ctl, bp, st) : 0;   // (k = 0: no block)
+    return bn == 0 ? launch_blk_publish(sh, s, p, bn, ctl, bp, st) : 0;   // (k = 0: no block)
 }
 
 bool block_args_ok(const smx_shape* shape, int k, int P, const void* blk, int64_t blk_bytes) {
@@ -1734,7 +1738,7 @@ int smx_bshard_run_timed(double* buf0, double* buf1, const smx_shape* shape, int
 int smx_bshard_prime(const double* T, const smx_shape* shape, int32_t parity, smx_ctl* ctl,
                      void* blk, int64_t blk_bytes, void* stream) {
     if (!bshard_args_ok(shape, 1, blk, blk_bytes) || !ctl) return (int)hipErrorInvalidValue;
-    return launch_blk_prime(T, *shape, parity & 1, parity & 1, ctl,
+    return launch_blk_prime(true, T, *shape, parity & 1, parity & 1, ctl,
                             blk_ptrs(*shape, static_cast<char*>(blk)), S(stream));
 }
 
@@ -1790,7 +1794,7 @@ int smx_bshard_sweep(double* Tin, double* Tother, const smx_shape* shape, int32_
     if (!bshard_args_ok(shape, pivots, blk, blk_bytes) || Tin == Tother)
         return (int)hipErrorInvalidValue;
     const BlkPtrs bp = blk_ptrs(*shape, static_cast<char*>(blk));
-    return launch_block_sweep(Tin, Tother, *shape, pivots, static_cast<char*>(blk), bp.L,
+    return launch_block_sweep(true, Tin, Tother, *shape, pivots, static_cast<char*>(blk), bp.L,
                               S(stream));
 }
 
@@ -1798,7 +1802,7 @@ int smx_bshard_publish(const smx_shape* shape, int32_t parity, int32_t block, sm
                        void* blk, int64_t blk_bytes, void* stream) {
     if (!bshard_args_ok(shape, 1, blk, blk_bytes) || !ctl || block < 0)
         return (int)hipErrorInvalidValue;
-    return launch_blk_publish(*shape, parity & 1, block, ctl,
+    return launch_blk_publish(true, *shape, parity & 1, block, ctl,
                               blk_ptrs(*shape, static_cast<char*>(blk)), S(stream));
 }
 
@@ -1891,7 +1895,7 @@ int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
     auto xrow = [&](int q) { return ranks[q].recv + (size_t)nranks * SMX_SHARD_HDR; };
     for (int q = 0; q < nranks && !err; ++q) {
         hipStream_t st = on(q);
-        err = launch_blk_prime(buf(q, parity & 1), ranks[q].shape, parity & 1, parity & 1,
+        err = launch_blk_prime(true, buf(q, parity & 1), ranks[q].shape, parity & 1, parity & 1,
                                ranks[q].ctl, bp[q], st);
     }
     int p = parity & 1, done = 0, bn = 0;
@@ -1988,14 +1992,14 @@ int mshard_enqueue(const smx_rank* ranks, int32_t nranks, int32_t parity, int32_
                                       light ? (int64_t)SMX_SHARD_HDR : 0);
         }
         for (int q = 0; q < nranks && !err; ++q)
-            err = launch_block_sweep(buf(q, p), buf(q, p ^ 1), ranks[q].shape, Pb,
+            err = launch_block_sweep(true, buf(q, p), buf(q, p ^ 1), ranks[q].shape, Pb,
                                      static_cast<char*>(ranks[q].blk), bp[q].L, on(q), 0, 0, p);
         p = (p + Pb) & 1;
         done += Pb;
         ++bn;
     }
     for (int q = 0; q < nranks && !err; ++q)
-        err = launch_blk_publish(ranks[q].shape, p, bn, ranks[q].ctl, bp[q], on(q));
+        err = launch_blk_publish(true, ranks[q].shape, p, bn, ranks[q].ctl, bp[q], on(q));
     if (!ev_ext) {
         for (int q = 0; q < 2 * nranks; ++q)
             if (ev[q]) {

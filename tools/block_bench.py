@@ -1,7 +1,8 @@
 """Per-pivot time of block pivots (smx_block_*: P pivots per HBM sweep) vs the fused one-pivot
 chain, on seeded uniform LPs, by tableau size and pivots per sweep.
 
-  python tools/block_bench.py [--sizes 4096,8192,16384] [--pivots 1,2,3,4,6,8] [--k 48] [--pipe 1,0]
+  python tools/block_bench.py [--sizes 4096,8192,16384] [--pivots 1,2,3,4,6,8] [--k 48]
+      [--planner 0,1] [--form 0]
 
 One JSON line per (size, path): us per pivot from HIP events on the solver stream around one
 graph replay of k pivots (after a warm-up replay), the average sweep time of a timed run
@@ -25,14 +26,11 @@ def main() -> None:
     ap.add_argument("--pivots", default="1,2,3,4,5,6,8")
     ap.add_argument("--k", type=int, default=48)
     ap.add_argument("--bpc", type=int, default=0, help="blocks per CU of the sweep (0: library)")
-    ap.add_argument("--pipe", default="0", help="smx_tune_block_pipe settings to compare, e.g. 1,0")
     ap.add_argument("--form", default="0", help="smx_tune_block_form settings to compare, e.g. 4,5")
-    ap.add_argument("--persist", default="0",
-                    help="smx_tune_block_persist settings to compare (planner: 0 one launch per "
-                         "pivot, 1 one persistent launch per block), e.g. 0,1")
-    ap.add_argument("--pipe-cus", default="0:0",
-                    help="smx_tune_block_pipe_cus settings (CUs per XCD : planner workgroup cap), "
-                         "e.g. 0:0,2:16,4:32 (with --pipe 0: the planner alone on those CUs)")
+    ap.add_argument("--planner", default="0",
+                    help="smx_tune_block_planner settings to compare (0 the window planner, 1 the "
+                         "register-form chains), e.g. 0,1")
+    ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -43,20 +41,15 @@ def main() -> None:
         _lib.check(_lib.load().smx_tune_set(-2, a.bpc), "smx_tune_set")
     for N in (int(x) for x in a.sizes.split(",")):
         n = m = N - 1
-        T = lp.dense_tableau("uniform", 0, n, m)
+        T = lp.dense_tableau("uniform", a.seed, n, m)
         dev = DeviceTableau(T, n, m, m, block=0)
         k = a.k
         ref_log = ref_tab = None
-        cus = [tuple(int(v) for v in c.split(":")) for c in a.pipe_cus.split(",")]
-        runs = [(0, 0, 0, 0, (0, 0))] + [(int(x), int(pp), int(f), int(ps), cu)
-                                         for x in a.pivots.split(",") for pp in a.pipe.split(",")
-                                         for f in a.form.split(",") for ps in a.persist.split(",")
-                                         for cu in cus]
-        for P, pipe, form, persist, cu in runs:
-            _lib.tune_block_pipe(pipe)
-            _lib.tune_block_pipe_cus(*cu)
+        runs = [(0, 0, 0)] + [(int(x), int(f), int(pl)) for x in a.pivots.split(",")
+                              for f in a.form.split(",") for pl in a.planner.split(",")]
+        for P, form, planner in runs:
             _lib.tune_block_form(form)
-            _lib.tune_block_persist(persist)
+            _lib.tune_block_planner(planner, 0)
             dev.close()   # captured graphs bake in the layout: capture afresh for every run
             dev.block = P
             dev.upload(T)
@@ -76,8 +69,8 @@ def main() -> None:
             ctl = dev.sync_state()
             log = dev.read_log(0, int(ctl["npivots"]))
             tab = dev.download().view(np.int64)
-            row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "pipe": pipe,
-                   "form": form, "persist": persist, "pipe_cus": list(cu), "k": k,
+            row = {"size": N, "path": "fused" if P == 0 else f"block{P}", "planner": planner,
+                   "form": form, "k": k,
                    "bpc": a.bpc,
                    "us_per_pivot": ms * 1e3 / k, "pivots_s": k / ms * 1e3,
                    "npivots": int(ctl["npivots"])}
@@ -86,10 +79,10 @@ def main() -> None:
             else:
                 row["same_as_fused"] = bool(np.array_equal(log, ref_log) and
                                             np.array_equal(tab, ref_tab))
-                for _ in range(2):   # an untimed eager run first: new (CU-masked) streams
-                    dev.upload(T)    # pay their first dispatches there
+                for _ in range(2):   # an untimed eager run first
+                    dev.upload(T)
                     dev.step = 0
-                    sw, tot = dev.run_block_timed(k, P)   # eager: CU partitions apply here only
+                    sw, tot = dev.run_block_timed(k, P)
                 ctl = dev.sync_state()
                 row["eager_same_as_fused"] = bool(
                     np.array_equal(dev.read_log(0, int(ctl["npivots"])), ref_log) and

@@ -8,7 +8,7 @@
 // Build (from the repo root):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DSMX_BLK_TRACE -Iinclude \
 //     -I/opt/rocm/include -L/opt/rocm/lib -lrccl tools/trace_planner.hip -o tools/trace_planner
-// Run: tools/trace_planner [N] [P] [blocks] [planner: 0 window (default), 1 register]
+// Run: tools/trace_planner [N] [P] [blocks] [planner: 0 window (default), 1 register] [nwin]
 #include "../simplex-method-solver_amd/csrc/smx_kernels.hip"
 
 #include <algorithm>
@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 16384;
     const int P = argc > 2 ? atoi(argv[2]) : 12;
     const int nblocks = argc > 3 ? atoi(argv[3]) : 3;
-    if (argc > 4) smx_tune_block_planner(atoi(argv[4]), 0);
+    if (argc > 4) smx_tune_block_planner(atoi(argv[4]), argc > 5 ? atoi(argv[5]) : 0);
     smx_shape s{};
     s.m = N - 1;
     s.n = s.rows = N - 1;
