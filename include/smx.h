@@ -353,11 +353,14 @@ int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear);
  * entries) and the chain's total. */
 int smx_tune_block(int32_t pivots);
 /* Planner of unsharded block chains: 0 (default) the window planner -- T_{k+D} at the first
- * nwin - 1 columns and the "-b" column of every row, kept current pivot by pivot, one launch per
- * pivot over up to 256 workgroups, the pivot rows at every column once per block (k_blk_wstep,
- * k_blk_prows; columns outside the window through chains from the block's input table); 1 the
- * register-form chains (k_blk_step).  nwin: window slots 2..64 (0 = 64, the default; -1 keeps
- * it).  Same decisions and bits either way.  Returns the previous planner. */
+ * nwin - 1 columns and the "-b" column of every row, kept current pivot by pivot over up to 256
+ * workgroups: ONE persistent launch per block (k_blk_wplan: the window in registers, the steps
+ * handing off through tagged granules) where its workgroups fit one per CU and its rows in
+ * registers (up to 32,768 rows), else one launch per pivot (k_blk_wstep); then the pivot rows at
+ * every column once per block (k_blk_prows; columns outside the window through chains from the
+ * block's input table); 2 the window planner's launch form always; 1 the register-form chains
+ * (k_blk_step).  nwin: window slots 2..64 (0 = 64, the default; -1 keeps it).  Same decisions
+ * and bits either way.  Returns the previous planner. */
 int smx_tune_block_planner(int32_t planner, int32_t nwin);
 /* Layout of the block sweep (k_blk_sweep, csrc/smx_block.hpp): 0 automatic (the default: pivot-
  * row slices in registers up to 12 pivots per sweep, in LDS shared by a workgroup's waves beyond,

@@ -102,8 +102,11 @@ constexpr int kWin = 64;
 // parity) | the register-form planner's column caches | the window planner's window.  Plan slot 1
 // of mul / pr is unused since the pipelined planner left (kept: the layout stays put).
 struct BlkLayout {
-    int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, win;
+    int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, win, xg;
 };
+// the persistent window planner's granules (smx_wplan.hpp wp_granules: records [2][256][8],
+// pivot rows [2][2 * 64 + 2 * kBlkMax])
+constexpr int64_t kBlkXgBytes = (2 * 256 * 8 + 2 * (2 * kWin + 2 * kBlkMax)) * 8;
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     (void)nparts;   // records sized for the widest planner (the window planner: up to 256)
@@ -119,7 +122,8 @@ inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     // then the register form's column caches (7 R doubles: unused [3][R], [2][R] T_{k+L}[i][cf],
     // [2][R] T_{k+L}[i][m]), then the window [2][R][kWin] (R = rows + 1: the f-row's too)
     L.win = blk_align(L.fr + 2 * ld * 8 + 7 * R * 8);
-    L.bytes = blk_align(L.win + (int64_t)2 * R * kWin * 8);
+    L.xg = blk_align(L.win + (int64_t)2 * R * kWin * 8);
+    L.bytes = blk_align(L.xg + kBlkXgBytes);
     return L;
 }
 
@@ -507,9 +511,13 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_start(const double* __restrict__
                                                       BlkHdr* __restrict__ h,
                                                       BlkHdr* __restrict__ h1,
                                                       double* __restrict__ fr,
-                                                      smx_part* __restrict__ parts) {
+                                                      smx_part* __restrict__ parts,
+                                                      uint64_t* __restrict__ xg) {
     __shared__ int s_tmp[kBlkNT / kWave];
     const int b = blockIdx.x, G = gridDim.x, tid = threadIdx.x;
+    // the persistent window planner's granules: tag 0 never matches (its tags are >= 2)
+    if (xg)
+        for (int t = b * kBlkNT + tid; t < (int)(kBlkXgBytes / 8); t += G * kBlkNT) xg[t] = 0;
     if (b == 0 && tid == 0) {
         h->loc = loc;
         h->np0 = ctl->npivots;

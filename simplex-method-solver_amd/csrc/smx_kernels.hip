@@ -53,6 +53,7 @@ static_assert(sizeof(smx_part) == 32, "smx_part layout");
 #include "smx_resident.hpp"
 #include "smx_block.hpp"
 #include "smx_window.hpp"
+#include "smx_wplan.hpp"
 #include "smx_host.hpp"
 #include "smx_intfirst.hpp"
 
@@ -538,17 +539,24 @@ struct BlkPtrs {
     BlkHdr* h[2];
     smx_part* parts;
     double *mul[2], *pr[2], *fr, *win;
+    uint64_t* xg;   // the persistent window planner's granules (k_blk_start zeroes them)
 };
-// smx_tune_block_planner: 0 (default) the window planner (k_blk_wstep, smx_window.hpp) on
-// unsharded chains, 1 the register-form chains (k_blk_step<L, false>); row-sharded chains always
-// run the register form (k_blk_step<L, true>).  g_block_nwin: window slots (2..kWin; tests shrink
+// smx_tune_block_planner: 0 (default) the window planner on unsharded chains -- one persistent
+// launch per block (k_blk_wplan, smx_wplan.hpp) where its workgroups fit one per CU and its rows
+// fit in registers, else one launch per pivot (k_blk_wstep, smx_window.hpp); 2 the window
+// planner's launch form always; 1 the register-form chains (k_blk_step<L, false>).  Row-sharded
+// chains always run the register form (k_blk_step<L, true>).  g_block_nwin: window slots (2..kWin; tests shrink
 // it to drive the window's fallbacks).
 int g_block_planner = 0;
 int g_block_nwin = kWin;
 // (sh: a row-sharded chain -- at world size 1 its shape is the whole table, so the shape alone
 // cannot tell)
 bool use_window(const smx_shape& s, bool sh) {
-    return !sh && g_block_planner == 0 && s.row0 == 0 && s.rows == s.n;
+    return !sh && g_block_planner != 1 && s.row0 == 0 && s.rows == s.n;
+}
+bool use_wplan(const smx_shape& s, bool sh) {
+    return use_window(s, sh) && g_block_planner == 0 && win_rpw(s.rows) <= kWpMaxRpw &&
+           win_groups(s.rows) <= num_cus();
 }
 
 // Planner workgroups of a chain (every launch of one chain uses the same count, since a step
@@ -568,6 +576,7 @@ BlkPtrs blk_ptrs(const smx_shape& s, char* blk) {
     b.parts = reinterpret_cast<smx_part*>(blk + b.L.parts);
     b.fr = reinterpret_cast<double*>(blk + b.L.fr);
     b.win = reinterpret_cast<double*>(blk + b.L.win);
+    b.xg = reinterpret_cast<uint64_t*>(blk + b.L.xg);
     return b;
 }
 
@@ -576,7 +585,7 @@ int launch_blk_prime(bool sh, const double* T, const smx_shape& s, int parity, i
                      const BlkPtrs& b, hipStream_t st) {
     hipLaunchKernelGGL(k_blk_start, dim3(blk_G(s, sh)), dim3(kBlkNT), 0, st, T, s.ld, s.rows, s.m,
                        fscan_of(s), parity, loc, s.row0, (const smx_ctl*)ctl, b.h[0], b.h[1],
-                       b.fr, b.parts);
+                       b.fr, b.parts, use_wplan(s, sh) ? b.xg : nullptr);
     return (int)hipGetLastError();
 }
 
@@ -593,6 +602,17 @@ int launch_blk_step(bool sh, int L, const double* T, const smx_shape& s, int P, 
 }
 
 // One window-planner launch (block bn, step L) and, after a block's last step, the pivot rows
+// One persistent window-planner launch: block bn's Pb steps (done: pivots of the chain before it)
+int launch_blk_wplan(const double* T, const smx_shape& s, int P, int parity, int bn, int done,
+                     smx_ctl* ctl, const BlkPtrs& b, int32_t* log, double* xhist,
+                     int64_t log_cap, hipStream_t st) {
+    hipLaunchKernelGGL(k_blk_wplan, dim3(win_groups(s.rows)), dim3(kWinNT), 0, st, T, s.ld,
+                       s.rows, s.m, s.flen, fscan_of(s), P, parity, bn, done, g_block_nwin,
+                       win_rpw(s.rows), ctl, b.h[0], b.parts, b.mul[0], b.xg, log, xhist,
+                       log_cap);
+    return (int)hipGetLastError();
+}
+
 // fromT: the chain's first step (the window is read from the table itself)
 int launch_blk_wstep(int L, const double* T, const smx_shape& s, int P, int parity, int bn,
                      smx_ctl* ctl, const BlkPtrs& b, int32_t* log, double* xhist, int64_t log_cap,
@@ -741,7 +761,10 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
         const int Pb = block_size(k, P, bn);
         double* tin = p ? buf1 : buf0;
         double* toth = p ? buf0 : buf1;
-        for (int l = 1; l <= Pb && !err; ++l) {
+        const bool wplan = use_wplan(s, sh);
+        if (!err && wplan)
+            err = launch_blk_wplan(tin, s, Pb, p, bn, done, ctl, bp, log, xhist, log_cap, st);
+        for (int l = 1; l <= Pb && !err && !wplan; ++l) {
             if (sh) {
                 err = launch_bsh_pack(l - 1, tin, s, Pb, bn, ctl, bp, send, st);
                 if (!err && !light) {
@@ -1539,7 +1562,7 @@ int smx_tune_block_form(int32_t form) {
 
 int smx_tune_block_planner(int32_t planner, int32_t nwin) {
     const int prev = g_block_planner;
-    if (planner == 0 || planner == 1) g_block_planner = planner;
+    if (planner >= 0 && planner <= 2) g_block_planner = planner;
     if (nwin >= 2 && nwin <= kWin) g_block_nwin = nwin;
     else if (nwin == 0) g_block_nwin = kWin;
     return prev;

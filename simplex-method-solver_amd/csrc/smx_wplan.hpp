@@ -1,0 +1,509 @@
+// smx_wplan.hpp -- the window planner as ONE persistent launch per block (k_blk_wplan).
+// Part of libsmx (compiled as one translation unit by smx_kernels.hip; not a standalone header).
+#pragma once
+#pragma clang fp contract(off)
+
+namespace {
+
+// Why.  The launch form of the window planner (k_blk_wstep, smx_window.hpp) pays per step a
+// kernel boundary (~1.5 us plus the dirty bytes it leaves: the window it rewrites, 8 MB at 16384
+// rows, MI355X_MICROARCH.md "boundary"), a full read and write of that window, and the record
+// round trip after every boundary: ~15 us per step at 16384^2 (profiles/r06i/).  Here every
+// workgroup keeps its rows' window in REGISTERS for the whole block and the steps hand off
+// through tagged 8-byte granules ({32-bit payload, 32-bit tag}, relaxed agent-scope = sc1 stores
+// and loads, the resident loop's protocol, smx_resident.hpp): per step every workgroup publishes
+// its 32-B record (8 granules), polls all of them, decides; the wave owning the pivot row
+// publishes that row's window and its multipliers (the fallbacks' operands); every wave applies
+// the pivot to its rows in registers.  No window traffic, no boundary; the pivots, multipliers,
+// log and x-history go out as in the launch form (plain stores, read after the kernel).
+// Co-residency: one workgroup per CU (G <= CUs, launched only then); every spin is bounded
+// (g_res_spin_ticks): a workgroup that times out latches kResTimeout in ctl->dec[0][0], stops
+// the chain and leaves at its next barrier, so the grid always drains, and the host reports it.
+constexpr int kWpRecG = 8;                       // granules per record (32 B of payload)
+constexpr int kWpRowG = 2 * kWin + 2 * kBlkMax;  // pivot row: window + multipliers (2 per double)
+constexpr int kWpMaxRpw = 16;                    // rows per wave held in registers at most (32,768 rows)
+
+// scratch (uint64 granules): records [2 parities][kWinMaxG][kWpRecG], pivot rows [2][kWpRowG]
+static_assert((2 * kWinMaxG * kWpRecG + 2 * kWpRowG) * 8 == kBlkXgBytes, "granule scratch");
+
+__device__ __forceinline__ uint64_t wp_tag(uint32_t epoch, int L) {
+    return (uint64_t)((epoch << 8) | (uint32_t)L) << 32;
+}
+
+// The pivot-row values of column j after the block's first D pivots (win_colvals with the
+// multipliers of pivot rows from `mp` -- LDS, [pivot][step] -- and extra rows' from `xm`)
+template <int NX, class OUT>
+__device__ __forceinline__ void wp_colvals(const double* __restrict__ T, int64_t ld, int j, int D,
+                                           const BlkPiv& pv, const double (*mp)[kBlkMax],
+                                           const int* xr, const double (*xm)[kBlkMax], OUT out,
+                                           double* xo) {
+    double x[kBlkMax];
+    double xx[NX > 0 ? NX : 1];
+#pragma unroll
+    for (int p = 0; p < kBlkMax; ++p) x[p] = p < D ? T[(int64_t)pv.r[p] * ld + j] : 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) xx[k] = T[(int64_t)xr[k] * ld + j];
+#pragma unroll 1
+    for (int q = 0; q < D; ++q) {
+        const double p = x[0];
+        out(q, p);
+        const int rq = pv.r[q];
+        const bool pc = j == pv.c[q];
+        const double e = pv.e[q];
+#pragma unroll
+        for (int s = 1; s < kBlkMax; ++s) {
+            const int t = q + s;
+            if (t < D) x[s] = win_upd(x[s], pv.r[t] == rq, pc, p, mp[t][q], e);
+        }
+#pragma unroll
+        for (int k = 0; k < NX; ++k) xx[k] = win_upd(xx[k], xr[k] == rq, pc, p, xm[k][q], e);
+#pragma unroll
+        for (int s = 0; s + 1 < kBlkMax; ++s) x[s] = x[s + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < NX; ++k) xo[k] = xx[k];
+}
+
+
+// One block of P planner steps in one launch.  Grid: win_groups(rows) workgroups of kWinNT
+// threads (<= one per CU), wave w owns rows [w rpw, (w + 1) rpw) (rpw <= kWpMaxRpw).  xg: the
+// granule scratch, zeroed by k_blk_start at every chain's start (tags are unique within a chain:
+// done + L + 1, `done` = pivots of the chain before this block).  The decisions, the arithmetic
+// and every output are the launch form's (k_blk_wstep), step for step.
+__global__ __launch_bounds__(kWinNT) void k_blk_wplan(
+    const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int P,
+    int parity, int bn, int done, int nwin, int rpw, smx_ctl* __restrict__ ctl,
+    BlkHdr* __restrict__ h, smx_part* __restrict__ parts, double* __restrict__ mul,
+    uint64_t* __restrict__ xg, int32_t* __restrict__ log, double* __restrict__ xhist,
+    int64_t log_cap) {
+    __shared__ BlkPiv s_pv;                      // the block's pivots so far (r, c, e)
+    __shared__ double s_mp[kBlkMax + 1][kBlkMax]; // [pivot t][step q]: mul[r_t][q], published
+    // the fallbacks' extra rows: [0] the current pivot row's multipliers, [1] the f-row's (fc_q)
+    __shared__ double s_xm[2][kBlkMax];
+    __shared__ Decision s_d;
+    __shared__ int s_nb, s_bail;
+    __shared__ double s_e, s_fc, s_prcf;
+    __shared__ double s_colc[kBlkMax], s_colf[kBlkMax];
+    __shared__ int s_tmp[kWinWaves];
+    __shared__ BlkRec s_r[kWinWaves];
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
+    const int b = blockIdx.x, G = gridDim.x;
+    const int C = m + 1;
+    const int jl = win_col(lane, nwin, C);
+    const int jc = max(jl, 0);
+    uint64_t* __restrict__ rec = xg;                                  // [2][kWinMaxG][kWpRecG]
+    uint64_t* __restrict__ prg = xg + 2 * (int64_t)kWinMaxG * kWpRecG; // [2][kWpRowG]
+    const int64_t spin = g_res_spin_ticks;
+    const int i0 = (b * kWinWaves + wid) * rpw;
+    const int i1 = min(rows, i0 + rpw);
+    constexpr int RU = kBlkPartsMax / kWave;
+    // The block's first records (built by the previous launch), the chain state, this wave's
+    // rows and the f-row at the window's columns from the table itself (T_k)
+    const int stopped = ctl->term;
+    smx_part rp[RU];
+    if (wid == 0) {
+        const smx_part* __restrict__ slot = parts + (int64_t)blk_slot(0, P, bn) * G;
+#pragma unroll
+        for (int u = 0; u < RU; ++u) rp[u] = slot[min(lane + u * kWave, G - 1)];
+    }
+    int cf = h->cfs[blk_slot(0, P, bn)];   // the entering column of block step 0
+    int hx0 = ctl->xpos[parity][0], hx1 = ctl->xpos[parity][1];
+    int64_t kpiv = ctl->npiv[parity];
+    asm volatile("" ::: "memory");
+    double x[kWpMaxRpw];
+#pragma unroll
+    for (int u = 0; u < kWpMaxRpw; ++u) {
+        if (u < rpw) {
+            const double v = T[(int64_t)(i0 + u < i1 ? i0 + u : rows) * ld + jc];
+            x[u] = jl >= 0 ? v : 0.0;
+        } else {
+            x[u] = 0.0;
+        }
+    }
+    double fo;
+    {
+        const double v = T[(int64_t)rows * ld + jc];
+        fo = jl >= 0 ? v : 0.0;
+    }
+    if (tid == 0) s_bail = 0;
+    if (stopped) {
+        if (b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
+        return;
+    }
+    const int ms = __builtin_amdgcn_readfirstlane(win_slot(m, nwin, C));
+    double* __restrict__ mT = blk_mulT(mul, rows + 1);
+    const bool want_x = xhist && log_cap > 0;
+    auto bail = [&](int D) {
+        // a hand-off that never came (a workgroup not resident or stalled): stop the chain; the
+        // host reports it (device.py sync_state, RESIDENT_TIMEOUT)
+        atomicOr(&ctl->dec[0][0], kResTimeout);
+        ctl->term = 1;
+        if (b == 0) h->peff = D;
+        s_bail = 1;
+    };
+#pragma unroll 1
+    for (int L = 1; L <= P; ++L) {
+        const int D = L - 1;
+        const int sp = (parity + D) & 1;
+        const uint64_t tagD = (uint64_t)(uint32_t)(done + D + 1) << 32;
+        const uint64_t tagL = (uint64_t)(uint32_t)(done + L + 1) << 32;
+        // ---- the records of step D: from memory at D = 0, else the granules of step D --------
+        if (wid == 0) {
+            if (D > 0) {
+                const uint64_t* src = rec + (int64_t)(D & 1) * kWinMaxG * kWpRecG;
+#pragma unroll
+                for (int u = 0; u < RU; ++u) {
+                    const int k = min(lane + u * kWave, G - 1);
+                    uint64_t w[kWpRecG];
+                    const int64_t t0 = rt_now();
+                    bool ok;
+                    do {
+#pragma unroll
+                        for (int g = 0; g < kWpRecG; ++g) w[g] = ld_sc1(src + (int64_t)k * kWpRecG + g);
+                        ok = true;
+#pragma unroll
+                        for (int g = 0; g < kWpRecG; ++g) ok = ok && (w[g] & 0xFFFFFFFF00000000ull) == tagD;
+                        if (!ok && rt_now() - t0 > spin) break;
+                    } while (!ok);
+                    if (!ok) bail(D);
+                    uint32_t pl[kWpRecG];
+#pragma unroll
+                    for (int g = 0; g < kWpRecG; ++g) pl[g] = (uint32_t)w[g];
+                    smx_part pt;
+                    __builtin_memcpy(&pt, pl, sizeof(pt));
+                    rp[u] = pt;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < RU; ++u)
+                if (lane + u * kWave >= G) rp[u] = smx_part{SMX_NONE, SMX_NONE, 0.0, 3, SMX_NONE, 0.0};
+            const int c = cf;
+            int n0 = SMX_NONE;
+            First fi{SMX_NONE, 0.0};
+            Cand bq = cand_none();
+#pragma unroll
+            for (int u = 0; u < RU; ++u) {
+                n0 = min(n0, rp[u].p1col);
+                if (rp[u].first < fi.idx) fi = First{rp[u].first, rp[u].first_v};
+                const Cand o{rp[u].best_cls, rp[u].best_i, rp[u].best_v};
+                if (better(o, bq)) bq = o;
+            }
+            const int nb = wave_min_int_dpp(n0);
+            const First f = wave_first_dpp(fi);
+            const Cand bb = wave_best_dpp(bq);
+            Decision d;
+            d.c = c;
+            d.r = SMX_NONE;
+            d.status = SMX_PIVOT;
+            if (nb == SMX_NONE) {          // phase 2 (the records were built for column c)
+                if (c == SMX_NONE) {
+                    d.status = (flen < m) ? SMX_FSHORT : SMX_OPTIMUM;   // simplex.py:101-103
+                } else if (f.idx == SMX_NONE) {
+                    d.status = SMX_NOT_CONVERGE;                       // simplex.py:138-139
+                } else if (isnan(f.v)) {
+                    d.r = f.idx;                                       // simplex.py:117-121
+                } else if (bb.cls >= 2) {
+                    d.status = SMX_NOT_CONVERGE;
+                } else {
+                    d.r = bb.idx;
+                }
+            } else {
+                d.r = nb;                  // phase 1: the column comes from row r below
+                d.c = SMX_NONE;
+            }
+            if (tid == 0) {
+                s_nb = nb;
+                s_d = d;
+            }
+        }
+        __syncthreads();
+        if (s_bail) return;
+        const int nb = s_nb;
+        Decision d = s_d;
+        auto terminal = [&](const Decision& dd) {
+            if (b == 0 && tid == 0) {
+                ctl->sel_status = dd.status;
+                ctl->sel_r = dd.r;
+                ctl->sel_c = dd.c;
+                ctl->negb[sp] = nb;        // the state of T_{k+D}, where the chain stops
+                ctl->negf[sp] = cf;
+                ctl->term = 1;
+                h->peff = D;
+            }
+        };
+        if (d.status != SMX_PIVOT) {
+            terminal(d);
+            return;
+        }
+        const int r = d.r;
+        // ---- the pivot row: its owner wave publishes its window and multipliers ---------------
+        uint64_t* __restrict__ prow = prg + (int64_t)(L & 1) * kWpRowG;
+        if (r >= i0 && r < i1) {
+            double v = 0.0;
+#pragma unroll
+            for (int u = 0; u < kWpMaxRpw; ++u)
+                if (u < rpw && i0 + u == r) v = x[u];
+            const uint64_t bits = dbits(v);
+            st_sc1(prow + 2 * lane, tagL | (uint32_t)bits);
+            st_sc1(prow + 2 * lane + 1, tagL | (uint32_t)(bits >> 32));
+            if (lane < D) {
+                // (stored by other lanes of this wave at earlier steps: an agent-scope load)
+                const uint64_t mb = ld_sc1(reinterpret_cast<const uint64_t*>(mul) +
+                                           (int64_t)r * kBlkMax + lane);
+                st_sc1(prow + 2 * kWin + 2 * lane, tagL | (uint32_t)mb);
+                st_sc1(prow + 2 * kWin + 2 * lane + 1, tagL | (uint32_t)(mb >> 32));
+            }
+        }
+        double pw;
+        {
+            const int64_t t0 = rt_now();
+            uint64_t lo, hi;
+            bool ok;
+            do {
+                lo = ld_sc1(prow + 2 * lane);
+                hi = ld_sc1(prow + 2 * lane + 1);
+                ok = __all((lo & 0xFFFFFFFF00000000ull) == tagL &&
+                           (hi & 0xFFFFFFFF00000000ull) == tagL);
+                if (!ok && rt_now() - t0 > spin) break;
+            } while (!ok);
+            if (!ok && lane == 0) bail(D);   // (the workgroup leaves at the barrier below)
+            const double v = bitsd((hi << 32) | (lo & 0xFFFFFFFFull));
+            pw = jl >= 0 ? v : 0.0;   // T_{k+D}[r][jl]
+        }
+        if (wid == 0 && lane < D) {   // row r's multipliers, for the fallbacks' chains
+            const int64_t t0 = rt_now();
+            uint64_t lo, hi;
+            for (;;) {
+                lo = ld_sc1(prow + 2 * kWin + 2 * lane);
+                hi = ld_sc1(prow + 2 * kWin + 2 * lane + 1);
+                if ((lo & 0xFFFFFFFF00000000ull) == tagL && (hi & 0xFFFFFFFF00000000ull) == tagL)
+                    break;
+                if (rt_now() - t0 > spin) {
+                    bail(D);
+                    break;
+                }
+            }
+            const double mv = bitsd((hi << 32) | (lo & 0xFFFFFFFFull));
+            s_mp[D][lane] = mv;
+            s_xm[0][lane] = mv;
+        }
+        if (tid == 0) {
+            s_pv.r[D] = r;
+            // (c, e below, before anything reads them)
+        }
+        __syncthreads();
+        if (s_bail) return;
+        int c = d.c;
+        if (nb != SMX_NONE) {
+            // phase 1: first j < m with T_{k+D}[r][j] > 0 (simplex.py:81-85)
+            const unsigned long long bal = __ballot(jl >= 0 && jl < m && pw > 0.0);
+            int p1 = bal ? win_col(__ffsll((long long)bal) - 1, nwin, C) : SMX_NONE;
+            if (p1 == SMX_NONE && C > nwin) {
+                const int xr[1] = {r};
+                for (int j0 = nwin - 1; j0 < m && p1 == SMX_NONE; j0 += kWinNT) {
+                    const int j = j0 + tid;
+                    int mine = SMX_NONE;
+                    if (j < m) {
+                        double xo[1];
+                        wp_colvals<1>(T, ld, j, D, s_pv, s_mp, xr, s_xm, [](int, double) {}, xo);
+                        if (xo[0] > 0.0) mine = j;
+                    }
+                    p1 = block_min_int_dpp<kWinNT>(mine, s_tmp);
+                }
+            }
+            if (p1 == SMX_NONE) {
+                d.c = SMX_NONE;
+                d.status = SMX_INCORRECT;  // simplex.py:88-89
+                terminal(d);
+                return;
+            }
+            c = p1;
+        }
+        // the pivot element and the f-row's multiplier
+        const int cs = __builtin_amdgcn_readfirstlane(win_slot(c, nwin, C));
+        double e, fc;
+        if (cs >= 0) {
+            e = readlane_d(pw, cs);
+            fc = readlane_d(fo, cs);
+        } else {
+            if (tid == 0) {
+                const int xr[2] = {r, rows};
+                double xo[2];
+                wp_colvals<2>(T, ld, c, D, s_pv, s_mp, xr, s_xm,
+                              [&](int q, double v) { s_colc[q] = v; }, xo);
+                s_e = xo[0];
+                s_fc = xo[1];
+            }
+            __syncthreads();
+            e = s_e;
+            fc = s_fc;
+        }
+        // the f-row after this pivot and the next entering column
+        const double fn = jl >= 0 ? win_upd(fo, false, jl == c, pw, fc, e) : 0.0;
+        int cfn;
+        {
+            const unsigned long long bal = __ballot(jl >= 0 && jl < fscan && fn < 0.0);
+            cfn = bal ? win_col(__ffsll((long long)bal) - 1, nwin, C) : SMX_NONE;
+            if (cfn == SMX_NONE && C > nwin) {
+                const int xr[2] = {r, rows};
+                for (int j0 = nwin - 1; j0 < fscan && cfn == SMX_NONE; j0 += kWinNT) {
+                    const int j = j0 + tid;
+                    int mine = SMX_NONE;
+                    if (j < fscan) {
+                        double xo[2];
+                        wp_colvals<2>(T, ld, j, D, s_pv, s_mp, xr, s_xm, [](int, double) {}, xo);
+                        if (win_upd(xo[1], false, j == c, xo[0], fc, e) < 0.0) mine = j;
+                    }
+                    cfn = block_min_int_dpp<kWinNT>(mine, s_tmp);
+                }
+            }
+        }
+        const int cfs = __builtin_amdgcn_readfirstlane(cfn != SMX_NONE ? win_slot(cfn, nwin, C) : -1);
+        if (cfn != SMX_NONE && cfs < 0) {
+            if (tid == 0) {
+                const int xr[1] = {r};
+                double xo[1];
+                wp_colvals<1>(T, ld, cfn, D, s_pv, s_mp, xr, s_xm,
+                              [&](int q, double v) { s_colf[q] = v; }, xo);
+                s_prcf = xo[0];
+            }
+            __syncthreads();
+        }
+        // bookkeeping of this pivot (workgroup 0), the labels in every workgroup (simplex.py:152)
+        hx0 = move_label(hx0, r, c);
+        hx1 = move_label(hx1, r, c);
+        if (b == 0 && tid == 0) {
+            const FastDiv fd = fd_prep(e);
+            mul[(int64_t)rows * kBlkMax + D] = fc;
+            h->r[D] = r;
+            h->c[D] = c;
+            h->e[D] = e;
+            h->y[D] = fd.y;
+            h->ok[D] = fd.ok ? 1 : 0;
+            h->peff = D + 1;
+            if (log_cap > 0) {
+                log[2 * (kpiv % log_cap)] = r;
+                log[2 * (kpiv % log_cap) + 1] = c;
+            }
+            ctl->npivots = kpiv + 1;
+            ctl->npiv[sp ^ 1] = kpiv + 1;
+            ctl->sel_status = SMX_PIVOT;
+            ctl->sel_r = r;
+            ctl->sel_c = c;
+            ctl->sel_e = e;
+            ctl->xpos[sp ^ 1][0] = hx0;
+            ctl->xpos[sp ^ 1][1] = hx1;
+            if (want_x) {                          // non-basic labels: 0 (simplex.py:60-66)
+                if (hx0 < 0) xhist[2 * (kpiv % log_cap)] = 0.0;
+                if (hx1 < 0) xhist[2 * (kpiv % log_cap) + 1] = 0.0;
+            }
+            if (L == P) h->cfs[blk_slot(L, P, bn)] = cfn;
+        }
+        const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
+        // the row pass (registers): every row of the wave through the pivot, its multiplier
+        // stored for the sweep, the records of step L on column cfn (k_blk_wstep's pass)
+        const FastDiv efd = fd_prep(e);
+        const double ey = efd.y;
+        const bool eok = efd.ok;
+        BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
+#pragma unroll
+        for (int ub = 0; ub < kWpMaxRpw; ub += kWinBatch) {
+            if (ub < rpw) {
+                const int ib = i0 + ub;
+                double mcv = 0.0, acv = 0.0;
+                if (cs < 0 && lane < kWinBatch && ib + lane < i1)
+                    mcv = win_chain(T, ld, ib + lane, c, D, s_pv, s_colc, mul);
+                if (cfs < 0 && cfn != SMX_NONE && lane < kWinBatch && ib + lane < i1)
+                    acv = win_chain(T, ld, ib + lane, cfn, D, s_pv, s_colf, mul);
+                double mc[kWinBatch], nv[kWinBatch];
+#pragma unroll
+                for (int u = 0; u < kWinBatch; ++u)
+                    mc[u] = __shfl(cs >= 0 ? x[ub + u] : mcv, cs >= 0 ? cs : u);
+                uint32_t wt = 0;
+#pragma unroll
+                for (int u = 0; u < kWinBatch; ++u) {
+                    const double a = x[ub + u] * e;
+                    const double bq = pw * mc[u];
+                    const bool pc = jl == c;
+                    const double num = (ib + u == r) ? (pc ? 1.0 : -x[ub + u]) : (pc ? x[ub + u] : (a - bq));
+                    wt = max(wt, win_term(num));
+                    const double tq = num * ey;
+                    const double rr = fma(-e, tq, num);
+                    nv[u] = fma(rr, ey, tq);
+                }
+                if (!eok || !__all(jl < 0 || wt < kWinSpan)) {
+#pragma unroll
+                    for (int u = 0; u < kWinBatch; ++u)
+                        nv[u] = win_upd(x[ub + u], ib + u == r, jl == c, pw, mc[u], e);
+                }
+#pragma unroll
+                for (int u = 0; u < kWinBatch; ++u) x[ub + u] = jl >= 0 ? nv[u] : 0.0;
+                double myc = 0.0, mybv = 0.0, mya = 0.0;
+#pragma unroll
+                for (int u = 0; u < kWinBatch; ++u) {
+                    const double bvu = __shfl(nv[u], ms);
+                    const double au = cfs >= 0 ? __shfl(nv[u], cfs) : 0.0;
+                    if (lane == u) {
+                        myc = mc[u];
+                        mybv = bvu;
+                        mya = au;
+                    }
+                }
+                const int i = ib + lane;
+                if (lane < kWinBatch && i < i1) {
+                    if (cfn != SMX_NONE && cfs < 0)
+                        mya = win_upd(acv, i == r, cfn == c, s_prcf, myc, e);
+                    mul[(int64_t)i * kBlkMax + D] = myc;
+                    mT[(int64_t)D * (rows + 1) + i] = myc;
+                    if (want_x) {
+                        if (i == hx0) xhist[hslot] = mybv;
+                        if (i == hx1) xhist[hslot + 1] = mybv;
+                    }
+                    blk_rec_add(R, i, mybv, cfn != SMX_NONE, mya);
+                }
+            }
+        }
+        // ---- the records of step L: granules (L < P) or memory (the next block's first) -------
+        {
+            const int n0 = wave_min_int_dpp(R.nb);
+            const First f0 = wave_first_dpp(R.f);
+            const Cand c0 = wave_best_dpp(R.bc);
+            if (lane == 0) s_r[wid] = BlkRec{n0, f0, c0};
+            if (tid == 0) {
+                s_pv.c[D] = c;
+                s_pv.e[D] = e;
+                s_xm[1][D] = fc;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (tid == 0) {
+                BlkRec a = s_r[0];
+                for (int w = 1; w < kWinWaves; ++w) {
+                    a.nb = min(a.nb, s_r[w].nb);
+                    if (s_r[w].f.idx < a.f.idx) a.f = s_r[w].f;
+                    if (better(s_r[w].bc, a.bc)) a.bc = s_r[w].bc;
+                }
+                smx_part pt;
+                pt.p1col = a.nb;
+                pt.first = a.f.idx;
+                pt.first_v = a.f.v;
+                pt.best_cls = a.bc.cls;
+                pt.best_i = a.bc.idx;
+                pt.best_v = a.bc.v;
+                if (L < P) {
+                    uint32_t pl[kWpRecG];
+                    __builtin_memcpy(pl, &pt, sizeof(pt));
+                    uint64_t* dst = rec + ((int64_t)(L & 1) * kWinMaxG + b) * kWpRecG;
+#pragma unroll
+                    for (int g = 0; g < kWpRecG; ++g) st_sc1(dst + g, tagL | pl[g]);
+                } else {
+                    parts[(int64_t)blk_slot(L, P, bn) * G + b] = pt;
+                }
+            }
+        }
+        fo = fn;
+        cf = cfn;
+        ++kpiv;
+    }
+}
+
+}  // namespace

@@ -303,8 +303,10 @@ def tune_block(pivots: int = -1) -> int:
 
 
 def tune_block_planner(planner: int = -1, nwin: int = -1) -> int:
-    """smx_tune_block_planner: 0 the window planner (the default), 1 the register-form chains, -1
-    query only; ``nwin`` window slots 2..64 (0: 64, -1: keep).  Returns the previous planner."""
+    """smx_tune_block_planner: 0 the window planner (the default: one persistent launch per block
+    where eligible, else one launch per pivot), 2 the window planner's launch form, 1 the
+    register-form chains, -1 query only; ``nwin`` window slots 2..64 (0: 64, -1: keep).  Returns
+    the previous planner."""
     return int(load().smx_tune_block_planner(planner, nwin))
 
 

@@ -23,10 +23,11 @@ def _need_gpu():
         pytest.skip("needs an MI355X")
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["window", "register"])
+@pytest.fixture(autouse=True, params=[0, 2, 1], ids=["wplan", "wstep", "register"])
 def planner_form(request):
-    """Every test twice: the window planner (k_blk_wstep, the default) and the register-form
-    chains (k_blk_step<L>, smx_tune_block_planner(1)) -- the same bits either way."""
+    """Every test three times: the window planner as one persistent launch per block (k_blk_wplan,
+    the default where eligible), the window planner's launch form (k_blk_wstep, planner 2) and the
+    register-form chains (k_blk_step<L>, planner 1) -- the same bits every way."""
     from simplex_mi355x import _lib
     prev = _lib.tune_block_planner(request.param, 0)
     yield request.param
@@ -98,9 +99,9 @@ def test_every_fixture_small_window(block_mode, planner_form, P, nwin):
     the block's input table) -- every trajectory fixture still equals the one-pivot chain and the
     reference's pivots."""
     from simplex_mi355x import _lib
-    if planner_form != 0:
+    if planner_form == 1:
         pytest.skip("window planner only")
-    _lib.tune_block_planner(0, nwin)
+    _lib.tune_block_planner(planner_form, nwin)
     n_blk = 0
     for label, cons, func, rec in CASES:
         if len(func) not in (len(cons[0]) - 1, len(cons[0])) or len(func) < 2:
@@ -131,9 +132,9 @@ def test_window_fallbacks_vs_oracle(block_mode, planner_form, kind, n, m, k, chu
     from oracle import c_oracle
     from simplex_mi355x import _lib, lp
     import simplex
-    if planner_form != 0:
+    if planner_form == 1:
         pytest.skip("window planner only")
-    _lib.tune_block_planner(0, nwin)
+    _lib.tune_block_planner(planner_form, nwin)
     block_mode(P)
     T = lp.dense_tableau(kind, 13, n, m)
     sm = simplex.SimplexMethod(T[:n].tolist(), T[n, :m].tolist())

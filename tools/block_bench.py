@@ -28,7 +28,8 @@ def main() -> None:
     ap.add_argument("--bpc", type=int, default=0, help="blocks per CU of the sweep (0: library)")
     ap.add_argument("--form", default="0", help="smx_tune_block_form settings to compare, e.g. 4,5")
     ap.add_argument("--planner", default="0",
-                    help="smx_tune_block_planner settings to compare (0 the window planner, 1 the "
+                    help="smx_tune_block_planner settings to compare (0 the window planner, persistent where "
+                         "eligible, 2 its launch form, 1 the "
                          "register-form chains), e.g. 0,1")
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
