@@ -104,9 +104,9 @@ constexpr int kWin = 64;
 struct BlkLayout {
     int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, win, xg;
 };
-// the persistent window planner's granules (smx_wplan.hpp wp_granules: records [2][256][8],
-// pivot rows [2][2 * 64 + 2 * kBlkMax])
-constexpr int64_t kBlkXgBytes = (2 * 256 * 8 + 2 * (2 * kWin + 2 * kBlkMax)) * 8;
+// the persistent window planner's granules (smx_wplan.hpp: records [2][256][4], pivot rows
+// [2][2 * 64 + 2 * kBlkMax])
+constexpr int64_t kBlkXgBytes = (2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax)) * 8;
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     (void)nparts;   // records sized for the widest planner (the window planner: up to 256)

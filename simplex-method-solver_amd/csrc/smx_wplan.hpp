@@ -19,16 +19,38 @@ namespace {
 // Co-residency: one workgroup per CU (G <= CUs, launched only then); every spin is bounded
 // (g_res_spin_ticks): a workgroup that times out latches kResTimeout in ctl->dec[0][0], stops
 // the chain and leaves at its next barrier, so the grid always drains, and the host reports it.
-constexpr int kWpRecG = 8;                       // granules per record (32 B of payload)
+// A record travels as 4 granules (16 B of payload): the three row indices in 16 bits each
+// (0xFFFF = none; eligible tables have at most 32,768 rows), the best candidate's class, whether
+// the first candidate's ratio is NaN (the only use of its value, the decision's simplex.py:117-121
+// test) and the best candidate's ratio -- a 16-KB all-gather per step instead of 32 KB.
+constexpr int kWpRecG = 4;
 constexpr int kWpRowG = 2 * kWin + 2 * kBlkMax;  // pivot row: window + multipliers (2 per double)
 constexpr int kWpMaxRpw = 16;                    // rows per wave held in registers at most (32,768 rows)
 
 // scratch (uint64 granules): records [2 parities][kWinMaxG][kWpRecG], pivot rows [2][kWpRowG]
 static_assert((2 * kWinMaxG * kWpRecG + 2 * kWpRowG) * 8 == kBlkXgBytes, "granule scratch");
 
-__device__ __forceinline__ uint64_t wp_tag(uint32_t epoch, int L) {
-    return (uint64_t)((epoch << 8) | (uint32_t)L) << 32;
+__device__ __forceinline__ uint32_t wp_idx16(int i) { return i == SMX_NONE ? 0xFFFFu : (uint32_t)i; }
+__device__ __forceinline__ int wp_idx(uint32_t v) { return v == 0xFFFFu ? SMX_NONE : (int)v; }
+__device__ __forceinline__ void wp_pack(const smx_part& pt, uint32_t* pl) {
+    pl[0] = wp_idx16(pt.p1col) | (wp_idx16(pt.first) << 16);
+    pl[1] = wp_idx16(pt.best_i) | ((uint32_t)pt.best_cls << 16) |
+            ((pt.first != SMX_NONE && isnan(pt.first_v)) ? 1u << 18 : 0u);
+    const uint64_t v = dbits(pt.best_v);
+    pl[2] = (uint32_t)v;
+    pl[3] = (uint32_t)(v >> 32);
 }
+__device__ __forceinline__ smx_part wp_unpack(const uint64_t* w) {
+    smx_part pt;
+    pt.p1col = wp_idx((uint32_t)w[0] & 0xFFFFu);
+    pt.first = wp_idx((uint32_t)w[0] >> 16);
+    pt.first_v = ((uint32_t)w[1] >> 18) & 1u ? __builtin_nan("") : 0.0;
+    pt.best_i = wp_idx((uint32_t)w[1] & 0xFFFFu);
+    pt.best_cls = (int)(((uint32_t)w[1] >> 16) & 3u);
+    pt.best_v = bitsd(((w[3] & 0xFFFFFFFFull) << 32) | (w[2] & 0xFFFFFFFFull));
+    return pt;
+}
+constexpr uint64_t kWpTagMask = 0xFFFFFFFF00000000ull;
 
 // The pivot-row values of column j after the block's first D pivots (win_colvals with the
 // multipliers of pivot rows from `mp` -- LDS, [pivot][step] -- and extra rows' from `xm`)
@@ -86,6 +108,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     __shared__ double s_colc[kBlkMax], s_colf[kBlkMax];
     __shared__ int s_tmp[kWinWaves];
     __shared__ BlkRec s_r[kWinWaves];
+    __shared__ double s_pw[kWave];               // the pivot row's window
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
     const int b = blockIdx.x, G = gridDim.x;
     const int C = m + 1;
@@ -143,6 +166,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     };
 #pragma unroll 1
     for (int L = 1; L <= P; ++L) {
+        SMX_BLK_STAMP(0);
         const int D = L - 1;
         const int sp = (parity + D) & 1;
         const uint64_t tagD = (uint64_t)(uint32_t)(done + D + 1) << 32;
@@ -150,29 +174,31 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         // ---- the records of step D: from memory at D = 0, else the granules of step D --------
         if (wid == 0) {
             if (D > 0) {
+                // every record at once (RU x 4 granule loads per lane in flight), again until all
+                // carry step D's tag
                 const uint64_t* src = rec + (int64_t)(D & 1) * kWinMaxG * kWpRecG;
+                uint64_t w[RU][kWpRecG];
+                const int64_t t0 = rt_now();
+                for (;;) {
 #pragma unroll
-                for (int u = 0; u < RU; ++u) {
-                    const int k = min(lane + u * kWave, G - 1);
-                    uint64_t w[kWpRecG];
-                    const int64_t t0 = rt_now();
-                    bool ok;
-                    do {
+                    for (int u = 0; u < RU; ++u)
 #pragma unroll
-                        for (int g = 0; g < kWpRecG; ++g) w[g] = ld_sc1(src + (int64_t)k * kWpRecG + g);
-                        ok = true;
+                        for (int g = 0; g < kWpRecG; ++g)
+                            w[u][g] = ld_sc1(src + (int64_t)min(lane + u * kWave, G - 1) * kWpRecG + g);
+                    bool ok = true;
 #pragma unroll
-                        for (int g = 0; g < kWpRecG; ++g) ok = ok && (w[g] & 0xFFFFFFFF00000000ull) == tagD;
-                        if (!ok && rt_now() - t0 > spin) break;
-                    } while (!ok);
-                    if (!ok) bail(D);
-                    uint32_t pl[kWpRecG];
+                    for (int u = 0; u < RU; ++u)
 #pragma unroll
-                    for (int g = 0; g < kWpRecG; ++g) pl[g] = (uint32_t)w[g];
-                    smx_part pt;
-                    __builtin_memcpy(&pt, pl, sizeof(pt));
-                    rp[u] = pt;
+                        for (int g = 0; g < kWpRecG; ++g) ok = ok && (w[u][g] & kWpTagMask) == tagD;
+                    if (__all(ok)) break;
+                    if (rt_now() - t0 > spin) {
+                        bail(D);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
+#pragma unroll
+                for (int u = 0; u < RU; ++u) rp[u] = wp_unpack(w[u]);
             }
 #pragma unroll
             for (int u = 0; u < RU; ++u)
@@ -216,7 +242,8 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 s_d = d;
             }
         }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // (LDS hand-off only)
+        SMX_BLK_STAMP(1);
         if (s_bail) return;
         const int nb = s_nb;
         Decision d = s_d;
@@ -254,45 +281,37 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 st_sc1(prow + 2 * kWin + 2 * lane + 1, tagL | (uint32_t)(mb >> 32));
             }
         }
-        double pw;
-        {
+        // one wave per workgroup polls the pivot row's window and multipliers into LDS
+        if (wid == 0) {
+            const bool wm = lane < D;   // row r's multipliers, for the fallbacks' chains
             const int64_t t0 = rt_now();
-            uint64_t lo, hi;
-            bool ok;
-            do {
+            uint64_t lo, hi, mlo = 0, mhi = 0;
+            for (;;) {
                 lo = ld_sc1(prow + 2 * lane);
                 hi = ld_sc1(prow + 2 * lane + 1);
-                ok = __all((lo & 0xFFFFFFFF00000000ull) == tagL &&
-                           (hi & 0xFFFFFFFF00000000ull) == tagL);
-                if (!ok && rt_now() - t0 > spin) break;
-            } while (!ok);
-            if (!ok && lane == 0) bail(D);   // (the workgroup leaves at the barrier below)
-            const double v = bitsd((hi << 32) | (lo & 0xFFFFFFFFull));
-            pw = jl >= 0 ? v : 0.0;   // T_{k+D}[r][jl]
-        }
-        if (wid == 0 && lane < D) {   // row r's multipliers, for the fallbacks' chains
-            const int64_t t0 = rt_now();
-            uint64_t lo, hi;
-            for (;;) {
-                lo = ld_sc1(prow + 2 * kWin + 2 * lane);
-                hi = ld_sc1(prow + 2 * kWin + 2 * lane + 1);
-                if ((lo & 0xFFFFFFFF00000000ull) == tagL && (hi & 0xFFFFFFFF00000000ull) == tagL)
-                    break;
+                mlo = ld_sc1(prow + 2 * kWin + 2 * lane);
+                mhi = ld_sc1(prow + 2 * kWin + 2 * lane + 1);
+                const bool ok = (lo & kWpTagMask) == tagL && (hi & kWpTagMask) == tagL &&
+                                (!wm || ((mlo & kWpTagMask) == tagL && (mhi & kWpTagMask) == tagL));
+                if (__all(ok)) break;
                 if (rt_now() - t0 > spin) {
-                    bail(D);
+                    bail(D);   // (the workgroup leaves at the barrier below)
                     break;
                 }
+                __builtin_amdgcn_s_sleep(1);
             }
-            const double mv = bitsd((hi << 32) | (lo & 0xFFFFFFFFull));
-            s_mp[D][lane] = mv;
-            s_xm[0][lane] = mv;
+            s_pw[lane] = bitsd((hi << 32) | (lo & 0xFFFFFFFFull));
+            if (wm) {
+                const double mv = bitsd((mhi << 32) | (mlo & 0xFFFFFFFFull));
+                s_mp[D][lane] = mv;
+                s_xm[0][lane] = mv;
+            }
+            if (lane == 0) s_pv.r[D] = r;   // (c, e below, before anything reads them)
         }
-        if (tid == 0) {
-            s_pv.r[D] = r;
-            // (c, e below, before anything reads them)
-        }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        SMX_BLK_STAMP(2);
         if (s_bail) return;
+        const double pw = jl >= 0 ? s_pw[lane] : 0.0;   // T_{k+D}[r][jl]
         int c = d.c;
         if (nb != SMX_NONE) {
             // phase 1: first j < m with T_{k+D}[r][j] > 0 (simplex.py:81-85)
@@ -358,6 +377,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 }
             }
         }
+        SMX_BLK_STAMP(3);
         const int cfs = __builtin_amdgcn_readfirstlane(cfn != SMX_NONE ? win_slot(cfn, nwin, C) : -1);
         if (cfn != SMX_NONE && cfs < 0) {
             if (tid == 0) {
@@ -399,6 +419,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
             }
             if (L == P) h->cfs[blk_slot(L, P, bn)] = cfn;
         }
+        SMX_BLK_STAMP(4);
         const int64_t hslot = 2 * (kpiv % (log_cap > 0 ? log_cap : 1));
         // the row pass (registers): every row of the wave through the pivot, its multiplier
         // stored for the sweep, the records of step L on column cfn (k_blk_wstep's pass)
@@ -463,6 +484,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 }
             }
         }
+        SMX_BLK_STAMP(5);
         // ---- the records of step L: granules (L < P) or memory (the next block's first) -------
         {
             const int n0 = wave_min_int_dpp(R.nb);
@@ -491,7 +513,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 pt.best_v = a.bc.v;
                 if (L < P) {
                     uint32_t pl[kWpRecG];
-                    __builtin_memcpy(pl, &pt, sizeof(pt));
+                    wp_pack(pt, pl);
                     uint64_t* dst = rec + ((int64_t)(L & 1) * kWinMaxG + b) * kWpRecG;
 #pragma unroll
                     for (int g = 0; g < kWpRecG; ++g) st_sc1(dst + g, tagL | pl[g]);
@@ -500,6 +522,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 }
             }
         }
+        SMX_BLK_STAMP(7);
         fo = fn;
         cf = cfn;
         ++kpiv;

@@ -8,7 +8,8 @@
 // Build (from the repo root):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DSMX_BLK_TRACE -Iinclude \
 //     -I/opt/rocm/include -L/opt/rocm/lib -lrccl tools/trace_planner.hip -o tools/trace_planner
-// Run: tools/trace_planner [N] [P] [blocks] [planner: 0 window (default), 1 register] [nwin]
+// Run: tools/trace_planner [N] [P] [blocks] [planner: 0 window (persistent where eligible,
+//   the default), 2 window launch form, 1 register] [nwin]
 #include "../simplex-method-solver_amd/csrc/smx_kernels.hip"
 
 #include <algorithm>
@@ -92,7 +93,7 @@ int main(int argc, char** argv) {
         }
         // the first kBlkTraceParts planner workgroups (window planner: phases 0 entry, 1 decision,
         // 2 pivot element, 3 next entering column, 4 bookkeeping, 5 row pass, 7 records stored)
-        const int Gp = g_block_planner == 0 ? win_groups(s.rows) : blk_parts_of(s.nparts, s.rows);
+        const int Gp = g_block_planner != 1 ? win_groups(s.rows) : blk_parts_of(s.nparts, s.rows);
         const int G = Gp < kBlkTraceParts ? Gp : kBlkTraceParts;
         unsigned long long prev_end = 0;
         for (int L = 1; L <= P; ++L) {
