@@ -104,9 +104,15 @@ constexpr int kWin = 64;
 struct BlkLayout {
     int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, win, xg;
 };
-// the persistent window planner's granules (smx_wplan.hpp: records [2][256][4], pivot rows
-// [2][2 * 64 + 2 * kBlkMax])
-constexpr int64_t kBlkXgBytes = (2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax)) * 8;
+// the persistent window planner's granules (smx_wplan.hpp: records [2][256][4], on-demand pivot
+// rows [2][2 * 64 + 2 * kBlkMax], every wave's candidate row [2][256 * 8][2 + 2 * 64 + 2 * kBlkMax])
+constexpr int64_t kBlkXgBytes =
+    (2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax) + 2 * 256 * 8 * (2 + 2 * kWin + 2 * kBlkMax)) * 8;
+// the granules a grid of G planner workgroups uses (the candidates stride by G * 8 waves): what
+// k_blk_start zeroes
+__host__ __device__ __forceinline__ int64_t blk_xg_used(int G) {
+    return 2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax) + (int64_t)2 * G * 8 * (2 + 2 * kWin + 2 * kBlkMax);
+}
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {
     (void)nparts;   // records sized for the widest planner (the window planner: up to 256)
@@ -517,7 +523,7 @@ __global__ __launch_bounds__(kBlkNT) void k_blk_start(const double* __restrict__
     const int b = blockIdx.x, G = gridDim.x, tid = threadIdx.x;
     // the persistent window planner's granules: tag 0 never matches (its tags are >= 2)
     if (xg)
-        for (int t = b * kBlkNT + tid; t < (int)(kBlkXgBytes / 8); t += G * kBlkNT) xg[t] = 0;
+        for (int64_t t = b * kBlkNT + tid; t < blk_xg_used(G); t += G * kBlkNT) xg[t] = 0;
     if (b == 0 && tid == 0) {
         h->loc = loc;
         h->np0 = ctl->npivots;
@@ -680,9 +686,11 @@ __global__ __launch_bounds__(kUpdBlock) void k_bsh_pick(const double* __restrict
 // Diagnostic build only (tools/trace_planner.hip): per-workgroup s_memrealtime stamps (100 MHz,
 // chip-wide) of every planner step, [block step L][workgroup][phase]: 0 entry, 1 decision known,
 // 2 pivot element known, 3 pivot-row / f-row slice written, 4 next entering column found,
-// 5 row pass operands staged, 6 row pass done, 7 records stored.
+// 5 row pass operands staged, 6 row pass done, 7 records stored (the persistent window planner:
+// 6 the LAST wave's row pass done, 8 after the records' workgroup barrier).
 constexpr int kBlkTraceParts = 64;
-__device__ unsigned long long g_blk_trace[kBlkMax + 1][kBlkTraceParts][8];
+constexpr int kBlkTracePh = 10;
+__device__ unsigned long long g_blk_trace[kBlkMax + 1][kBlkTraceParts][kBlkTracePh];
 #define SMX_BLK_STAMP_AT(ph)                                                           \
     do {                                                                               \
         if (threadIdx.x == 0 && blockIdx.x < kBlkTraceParts)                           \
@@ -694,6 +702,13 @@ __device__ unsigned g_blk_fallback[kBlkMax + 1][2];
 #define SMX_BLK_FALLBACK(k)                                                            \
     do {                                                                               \
         if ((threadIdx.x & (kWave - 1)) == 0) atomicAdd(&g_blk_fallback[L][k], 1u);    \
+    } while (0)
+// the latest of the workgroup's waves
+#define SMX_BLK_STAMP_WMAX(ph)                                                         \
+    do {                                                                               \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < kBlkTraceParts)                    \
+            atomicMax(&g_blk_trace[L][blockIdx.x][ph],                                 \
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());           \
     } while (0)
 #ifdef SMX_BLK_TRACE_P2
 // phase-2 anatomy instead: 2 operands landed, 3 fast chains done, 4 after the exact fallback
@@ -717,6 +732,9 @@ __device__ unsigned g_blk_fallback[kBlkMax + 1][2];
     } while (0)
 #define SMX_BLK_STAMP(ph) \
     do {                  \
+    } while (0)
+#define SMX_BLK_STAMP_WMAX(ph) \
+    do {                       \
     } while (0)
 #endif
 

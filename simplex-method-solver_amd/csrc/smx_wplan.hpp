@@ -8,37 +8,50 @@ namespace {
 // Why.  The launch form of the window planner (k_blk_wstep, smx_window.hpp) pays per step a
 // kernel boundary (~1.5 us plus the dirty bytes it leaves: the window it rewrites, 8 MB at 16384
 // rows, MI355X_MICROARCH.md "boundary"), a full read and write of that window, and the record
-// round trip after every boundary: ~15 us per step at 16384^2 (profiles/r06i/).  Here every
+// round trip after every boundary: ~13.7 us per step at 16384^2 (profiles/r06l/).  Here every
 // workgroup keeps its rows' window in REGISTERS for the whole block and the steps hand off
 // through tagged 8-byte granules ({32-bit payload, 32-bit tag}, relaxed agent-scope = sc1 stores
-// and loads, the resident loop's protocol, smx_resident.hpp): per step every workgroup publishes
-// its 32-B record (8 granules), polls all of them, decides; the wave owning the pivot row
-// publishes that row's window and its multipliers (the fallbacks' operands); every wave applies
-// the pivot to its rows in registers.  No window traffic, no boundary; the pivots, multipliers,
-// log and x-history go out as in the launch form (plain stores, read after the kernel).
-// Co-residency: one workgroup per CU (G <= CUs, launched only then); every spin is bounded
-// (g_res_spin_ticks): a workgroup that times out latches kResTimeout in ctl->dec[0][0], stops
-// the chain and leaves at its next barrier, so the grid always drains, and the host reports it.
+// and loads, the resident loop's protocol, smx_resident.hpp).  Per step:
+//   * every workgroup publishes its record (4 granules) and every wave publishes its CANDIDATE
+//     pivot row -- the row its own record would nominate (phase 1: its first row with a negative
+//     "-b"; phase 2: its ratio-test winner, or its first candidate when that ratio is NaN) -- with
+//     that row's window and multipliers, as soon as its row pass is done;
+//   * one wave per workgroup polls all records, decides (every workgroup identically), then
+//     fetches the winner's window from the owning wave's candidate slot -- one more round trip,
+//     the bytes already published.  Where the owner's candidate is another row (a NaN first
+//     candidate, the block's first step) the owner publishes the pivot row on demand instead;
+//   * every wave applies the pivot to its rows in registers.
+// No window traffic, no boundary; the pivots, multipliers, log and x-history go out as in the
+// launch form (plain stores, read after the kernel).  Co-residency: one workgroup per CU (G <=
+// CUs, launched only then); every spin is bounded (g_res_spin_ticks): a workgroup that times out
+// latches kResTimeout in ctl->dec[0][0], stops the chain and leaves at its next barrier, so the
+// grid always drains, and the host reports it.
 // A record travels as 4 granules (16 B of payload): the three row indices in 16 bits each
 // (0xFFFF = none; eligible tables have at most 32,768 rows), the best candidate's class, whether
 // the first candidate's ratio is NaN (the only use of its value, the decision's simplex.py:117-121
-// test) and the best candidate's ratio -- a 16-KB all-gather per step instead of 32 KB.
+// test) and the best candidate's ratio.
 constexpr int kWpRecG = 4;
-constexpr int kWpRowG = 2 * kWin + 2 * kBlkMax;  // pivot row: window + multipliers (2 per double)
-constexpr int kWpMaxRpw = 16;                    // rows per wave held in registers at most (32,768 rows)
+constexpr int kWpRowG = 2 * kWin + 2 * kBlkMax;       // on-demand pivot row: window, multipliers
+constexpr int kWpCandG = 2 + 2 * kWin + 2 * kBlkMax;  // a wave's candidate: row, window, mults
+constexpr int kWpMaxRpw = 16;                         // rows per wave in registers (32,768 rows)
+constexpr int kWpMaxWaves = kWinMaxG * kWinWaves;
 
-// scratch (uint64 granules): records [2 parities][kWinMaxG][kWpRecG], pivot rows [2][kWpRowG]
-static_assert((2 * kWinMaxG * kWpRecG + 2 * kWpRowG) * 8 == kBlkXgBytes, "granule scratch");
+// scratch (uint64 granules): records [2 parities][kWinMaxG][kWpRecG], on-demand pivot rows
+// [2][kWpRowG], candidates [2][G * kWinWaves][kWpCandG] (blk_xg_used(G) of them)
+static_assert((2 * kWinMaxG * kWpRecG + 2 * kWpRowG + 2 * kWpMaxWaves * kWpCandG) * 8 ==
+                  kBlkXgBytes,
+              "granule scratch");
+static_assert(kWinWaves == 8, "blk_xg_used");
 
 __device__ __forceinline__ uint32_t wp_idx16(int i) { return i == SMX_NONE ? 0xFFFFu : (uint32_t)i; }
 __device__ __forceinline__ int wp_idx(uint32_t v) { return v == 0xFFFFu ? SMX_NONE : (int)v; }
-__device__ __forceinline__ void wp_pack(const smx_part& pt, uint32_t* pl) {
-    pl[0] = wp_idx16(pt.p1col) | (wp_idx16(pt.first) << 16);
-    pl[1] = wp_idx16(pt.best_i) | ((uint32_t)pt.best_cls << 16) |
-            ((pt.first != SMX_NONE && isnan(pt.first_v)) ? 1u << 18 : 0u);
-    const uint64_t v = dbits(pt.best_v);
-    pl[2] = (uint32_t)v;
-    pl[3] = (uint32_t)(v >> 32);
+__device__ __forceinline__ uint32_t wp_pack1(const BlkRec& a, int g) {
+    if (g == 0) return wp_idx16(a.nb) | (wp_idx16(a.f.idx) << 16);
+    if (g == 1)
+        return wp_idx16(a.bc.idx) | ((uint32_t)a.bc.cls << 16) |
+               ((a.f.idx != SMX_NONE && isnan(a.f.v)) ? 1u << 18 : 0u);
+    const uint64_t v = dbits(a.bc.v);
+    return g == 2 ? (uint32_t)v : (uint32_t)(v >> 32);
 }
 __device__ __forceinline__ smx_part wp_unpack(const uint64_t* w) {
     smx_part pt;
@@ -51,6 +64,34 @@ __device__ __forceinline__ smx_part wp_unpack(const uint64_t* w) {
     return pt;
 }
 constexpr uint64_t kWpTagMask = 0xFFFFFFFF00000000ull;
+__device__ __forceinline__ bool wp_tagged(uint64_t w, uint64_t tag) { return (w & kWpTagMask) == tag; }
+__device__ __forceinline__ double wp_val(uint64_t lo, uint64_t hi) {
+    return bitsd((hi << 32) | (lo & 0xFFFFFFFFull));
+}
+__device__ __forceinline__ void wp_put(uint64_t* p, uint64_t tag, double v) {
+    const uint64_t bits = dbits(v);
+    st_sc1(p, tag | (uint32_t)bits);
+    st_sc1(p + 1, tag | (uint32_t)(bits >> 32));
+}
+// Branches a step almost never takes (fallbacks for columns outside the window, the exact
+// division's redo, time-outs, terminal steps): laid out after the hot path
+#define WP_COLD(x) __builtin_expect(!!(x), 0)
+
+// Records of the 8 waves (lanes 0..7 of wave 0, one each): merged in every lane of the group
+template <int CTRL>
+__device__ __forceinline__ BlkRec wp_rec_dpp(const BlkRec& a) {
+    BlkRec o;
+    o.nb = dpp_i<CTRL>(a.nb);
+    o.f = dpp_first<CTRL>(a.f);
+    o.bc = dpp_cand<CTRL>(a.bc);
+    return o;
+}
+__device__ __forceinline__ BlkRec wp_rec_merge(BlkRec a, const BlkRec& o) {
+    a.nb = min(a.nb, o.nb);
+    if (o.f.idx < a.f.idx) a.f = o.f;
+    if (better(o.bc, a.bc)) a.bc = o.bc;
+    return a;
+}
 
 // The pivot-row values of column j after the block's first D pivots (win_colvals with the
 // multipliers of pivot rows from `mp` -- LDS, [pivot][step] -- and extra rows' from `xm`)
@@ -86,7 +127,6 @@ __device__ __forceinline__ void wp_colvals(const double* __restrict__ T, int64_t
     for (int k = 0; k < NX; ++k) xo[k] = xx[k];
 }
 
-
 // One block of P planner steps in one launch.  Grid: win_groups(rows) workgroups of kWinNT
 // threads (<= one per CU), wave w owns rows [w rpw, (w + 1) rpw) (rpw <= kWpMaxRpw).  xg: the
 // granule scratch, zeroed by k_blk_start at every chain's start (tags are unique within a chain:
@@ -99,9 +139,12 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     uint64_t* __restrict__ xg, int32_t* __restrict__ log, double* __restrict__ xhist,
     int64_t log_cap) {
     __shared__ BlkPiv s_pv;                      // the block's pivots so far (r, c, e)
-    __shared__ double s_mp[kBlkMax + 1][kBlkMax]; // [pivot t][step q]: mul[r_t][q], published
+    __shared__ double s_mp[kBlkMax + 1][kBlkMax]; // [pivot t][step q]: mul[r_t][q]
     // the fallbacks' extra rows: [0] the current pivot row's multipliers, [1] the f-row's (fc_q)
     __shared__ double s_xm[2][kBlkMax];
+    // this workgroup's rows' multipliers [wave][row][step] (the candidates' and the on-demand
+    // pivot rows' multipliers come from here, not from a global round trip)
+    __shared__ double s_mrow[kWinWaves][kWpMaxRpw][kBlkMax];
     __shared__ Decision s_d;
     __shared__ int s_nb, s_bail;
     __shared__ double s_e, s_fc, s_prcf;
@@ -114,10 +157,13 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     const int C = m + 1;
     const int jl = win_col(lane, nwin, C);
     const int jc = max(jl, 0);
-    uint64_t* __restrict__ rec = xg;                                  // [2][kWinMaxG][kWpRecG]
-    uint64_t* __restrict__ prg = xg + 2 * (int64_t)kWinMaxG * kWpRecG; // [2][kWpRowG]
+    uint64_t* __restrict__ rec = xg;                                    // [2][kWinMaxG][kWpRecG]
+    uint64_t* __restrict__ prg = rec + 2 * (int64_t)kWinMaxG * kWpRecG;  // [2][kWpRowG]
+    uint64_t* __restrict__ cand = prg + 2 * (int64_t)kWpRowG;           // [2][waves][kWpCandG]
     const int64_t spin = g_res_spin_ticks;
-    const int i0 = (b * kWinWaves + wid) * rpw;
+    const int gw = b * kWinWaves + wid;   // this wave's index in the grid
+    const int NW = G * kWinWaves;
+    const int i0 = gw * rpw;
     const int i1 = min(rows, i0 + rpw);
     constexpr int RU = kBlkPartsMax / kWave;
     // The block's first records (built by the previous launch), the chain state, this wave's
@@ -149,7 +195,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         fo = jl >= 0 ? v : 0.0;
     }
     if (tid == 0) s_bail = 0;
-    if (stopped) {
+    if (WP_COLD(stopped)) {
         if (b == 0 && tid == 0) h->peff = 0;   // a later block of a stopped chain
         return;
     }
@@ -163,6 +209,15 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         ctl->term = 1;
         if (b == 0) h->peff = D;
         s_bail = 1;
+    };
+    // the row of x[] this wave published as its candidate for the coming step (none yet)
+    int mycand = SMX_NONE;
+    auto xrow = [&](int u) {   // x[u] for a uniform u
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < kWpMaxRpw; ++k)
+            if (k == u) v = x[k];
+        return v;
     };
 #pragma unroll 1
     for (int L = 1; L <= P; ++L) {
@@ -189,9 +244,9 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
 #pragma unroll
                     for (int u = 0; u < RU; ++u)
 #pragma unroll
-                        for (int g = 0; g < kWpRecG; ++g) ok = ok && (w[u][g] & kWpTagMask) == tagD;
+                        for (int g = 0; g < kWpRecG; ++g) ok = ok && wp_tagged(w[u][g], tagD);
                     if (__all(ok)) break;
-                    if (rt_now() - t0 > spin) {
+                    if (WP_COLD(rt_now() - t0 > spin)) {
                         bail(D);
                         break;
                     }
@@ -244,7 +299,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // (LDS hand-off only)
         SMX_BLK_STAMP(1);
-        if (s_bail) return;
+        if (WP_COLD(s_bail)) return;
         const int nb = s_nb;
         Decision d = s_d;
         auto terminal = [&](const Decision& dd) {
@@ -258,51 +313,68 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 h->peff = D;
             }
         };
-        if (d.status != SMX_PIVOT) {
+        if (WP_COLD(d.status != SMX_PIVOT)) {
             terminal(d);
             return;
         }
         const int r = d.r;
-        // ---- the pivot row: its owner wave publishes its window and multipliers ---------------
+        // ---- the pivot row: the owner's candidate slot, or published on demand -----------------
         uint64_t* __restrict__ prow = prg + (int64_t)(L & 1) * kWpRowG;
-        if (r >= i0 && r < i1) {
-            double v = 0.0;
-#pragma unroll
-            for (int u = 0; u < kWpMaxRpw; ++u)
-                if (u < rpw && i0 + u == r) v = x[u];
-            const uint64_t bits = dbits(v);
-            st_sc1(prow + 2 * lane, tagL | (uint32_t)bits);
-            st_sc1(prow + 2 * lane + 1, tagL | (uint32_t)(bits >> 32));
-            if (lane < D) {
-                // (stored by other lanes of this wave at earlier steps: an agent-scope load)
-                const uint64_t mb = ld_sc1(reinterpret_cast<const uint64_t*>(mul) +
-                                           (int64_t)r * kBlkMax + lane);
-                st_sc1(prow + 2 * kWin + 2 * lane, tagL | (uint32_t)mb);
-                st_sc1(prow + 2 * kWin + 2 * lane + 1, tagL | (uint32_t)(mb >> 32));
-            }
+        if (WP_COLD(r >= i0 && r < i1 && (D == 0 || mycand != r))) {
+            const int u = r - i0;
+            wp_put(prow + 2 * lane, tagL, xrow(u));
+            if (lane < D) wp_put(prow + 2 * kWin + 2 * lane, tagL, s_mrow[wid][u][lane]);
         }
-        // one wave per workgroup polls the pivot row's window and multipliers into LDS
         if (wid == 0) {
             const bool wm = lane < D;   // row r's multipliers, for the fallbacks' chains
             const int64_t t0 = rt_now();
-            uint64_t lo, hi, mlo = 0, mhi = 0;
-            for (;;) {
-                lo = ld_sc1(prow + 2 * lane);
-                hi = ld_sc1(prow + 2 * lane + 1);
-                mlo = ld_sc1(prow + 2 * kWin + 2 * lane);
-                mhi = ld_sc1(prow + 2 * kWin + 2 * lane + 1);
-                const bool ok = (lo & kWpTagMask) == tagL && (hi & kWpTagMask) == tagL &&
-                                (!wm || ((mlo & kWpTagMask) == tagL && (mhi & kWpTagMask) == tagL));
-                if (__all(ok)) break;
-                if (rt_now() - t0 > spin) {
-                    bail(D);   // (the workgroup leaves at the barrier below)
-                    break;
+            uint64_t lo = 0, hi = 0, mlo = 0, mhi = 0;
+            bool demand = D == 0;
+            if (!demand) {
+                const uint64_t* cs_ = cand + ((int64_t)(D & 1) * NW + r / rpw) * kWpCandG;
+                for (;;) {
+                    const uint64_t rg = ld_sc1(cs_);
+                    lo = ld_sc1(cs_ + 2 + 2 * lane);
+                    hi = ld_sc1(cs_ + 3 + 2 * lane);
+                    mlo = ld_sc1(cs_ + 2 + 2 * kWin + 2 * lane);
+                    mhi = ld_sc1(cs_ + 3 + 2 * kWin + 2 * lane);
+                    const uint32_t rtag = __builtin_amdgcn_readfirstlane((uint32_t)(rg >> 32));
+                    const uint32_t rrow = __builtin_amdgcn_readfirstlane((uint32_t)rg);
+                    if (rtag == (uint32_t)(tagD >> 32)) {
+                        if (rrow != (uint32_t)r) {   // the owner's candidate is another row
+                            demand = true;
+                            break;
+                        }
+                        const bool ok = wp_tagged(lo, tagD) && wp_tagged(hi, tagD) &&
+                                        (!wm || (wp_tagged(mlo, tagD) && wp_tagged(mhi, tagD)));
+                        if (__all(ok)) break;
+                    }
+                    if (WP_COLD(rt_now() - t0 > spin)) {
+                        bail(D);   // (the workgroup leaves at the barrier below)
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                __builtin_amdgcn_s_sleep(1);
             }
-            s_pw[lane] = bitsd((hi << 32) | (lo & 0xFFFFFFFFull));
+            if (WP_COLD(demand)) {
+                for (;;) {
+                    lo = ld_sc1(prow + 2 * lane);
+                    hi = ld_sc1(prow + 2 * lane + 1);
+                    mlo = ld_sc1(prow + 2 * kWin + 2 * lane);
+                    mhi = ld_sc1(prow + 2 * kWin + 2 * lane + 1);
+                    const bool ok = wp_tagged(lo, tagL) && wp_tagged(hi, tagL) &&
+                                    (!wm || (wp_tagged(mlo, tagL) && wp_tagged(mhi, tagL)));
+                    if (__all(ok)) break;
+                    if (WP_COLD(rt_now() - t0 > spin)) {
+                        bail(D);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            s_pw[lane] = wp_val(lo, hi);
             if (wm) {
-                const double mv = bitsd((mhi << 32) | (mlo & 0xFFFFFFFFull));
+                const double mv = wp_val(mlo, mhi);
                 s_mp[D][lane] = mv;
                 s_xm[0][lane] = mv;
             }
@@ -310,14 +382,14 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         SMX_BLK_STAMP(2);
-        if (s_bail) return;
+        if (WP_COLD(s_bail)) return;
         const double pw = jl >= 0 ? s_pw[lane] : 0.0;   // T_{k+D}[r][jl]
         int c = d.c;
         if (nb != SMX_NONE) {
             // phase 1: first j < m with T_{k+D}[r][j] > 0 (simplex.py:81-85)
             const unsigned long long bal = __ballot(jl >= 0 && jl < m && pw > 0.0);
             int p1 = bal ? win_col(__ffsll((long long)bal) - 1, nwin, C) : SMX_NONE;
-            if (p1 == SMX_NONE && C > nwin) {
+            if (WP_COLD(p1 == SMX_NONE && C > nwin)) {
                 const int xr[1] = {r};
                 for (int j0 = nwin - 1; j0 < m && p1 == SMX_NONE; j0 += kWinNT) {
                     const int j = j0 + tid;
@@ -330,7 +402,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                     p1 = block_min_int_dpp<kWinNT>(mine, s_tmp);
                 }
             }
-            if (p1 == SMX_NONE) {
+            if (WP_COLD(p1 == SMX_NONE)) {
                 d.c = SMX_NONE;
                 d.status = SMX_INCORRECT;  // simplex.py:88-89
                 terminal(d);
@@ -341,7 +413,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         // the pivot element and the f-row's multiplier
         const int cs = __builtin_amdgcn_readfirstlane(win_slot(c, nwin, C));
         double e, fc;
-        if (cs >= 0) {
+        if (__builtin_expect(cs >= 0, 1)) {
             e = readlane_d(pw, cs);
             fc = readlane_d(fo, cs);
         } else {
@@ -363,7 +435,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         {
             const unsigned long long bal = __ballot(jl >= 0 && jl < fscan && fn < 0.0);
             cfn = bal ? win_col(__ffsll((long long)bal) - 1, nwin, C) : SMX_NONE;
-            if (cfn == SMX_NONE && C > nwin) {
+            if (WP_COLD(cfn == SMX_NONE && C > nwin)) {
                 const int xr[2] = {r, rows};
                 for (int j0 = nwin - 1; j0 < fscan && cfn == SMX_NONE; j0 += kWinNT) {
                     const int j = j0 + tid;
@@ -379,7 +451,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         }
         SMX_BLK_STAMP(3);
         const int cfs = __builtin_amdgcn_readfirstlane(cfn != SMX_NONE ? win_slot(cfn, nwin, C) : -1);
-        if (cfn != SMX_NONE && cfs < 0) {
+        if (WP_COLD(cfn != SMX_NONE && cfs < 0)) {
             if (tid == 0) {
                 const int xr[1] = {r};
                 double xo[1];
@@ -429,17 +501,22 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
 #pragma unroll
         for (int ub = 0; ub < kWpMaxRpw; ub += kWinBatch) {
-            if (ub < rpw) {
+            if (ub == 0 || WP_COLD(ub < rpw)) {   // (a second batch from 16,385 rows on)
                 const int ib = i0 + ub;
                 double mcv = 0.0, acv = 0.0;
-                if (cs < 0 && lane < kWinBatch && ib + lane < i1)
+                if (WP_COLD(cs < 0) && lane < kWinBatch && ib + lane < i1)
                     mcv = win_chain(T, ld, ib + lane, c, D, s_pv, s_colc, mul);
-                if (cfs < 0 && cfn != SMX_NONE && lane < kWinBatch && ib + lane < i1)
+                if (WP_COLD(cfs < 0 && cfn != SMX_NONE) && lane < kWinBatch && ib + lane < i1)
                     acv = win_chain(T, ld, ib + lane, cfn, D, s_pv, s_colf, mul);
+                // row u's multiplier T_{k+D}[ib + u][c]: lane cs of x (uniform), or the chain
                 double mc[kWinBatch], nv[kWinBatch];
+                if (__builtin_expect(cs >= 0, 1)) {
 #pragma unroll
-                for (int u = 0; u < kWinBatch; ++u)
-                    mc[u] = __shfl(cs >= 0 ? x[ub + u] : mcv, cs >= 0 ? cs : u);
+                    for (int u = 0; u < kWinBatch; ++u) mc[u] = readlane_d(x[ub + u], cs);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kWinBatch; ++u) mc[u] = __shfl(mcv, u);
+                }
                 uint32_t wt = 0;
 #pragma unroll
                 for (int u = 0; u < kWinBatch; ++u) {
@@ -452,18 +529,20 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                     const double rr = fma(-e, tq, num);
                     nv[u] = fma(rr, ey, tq);
                 }
-                if (!eok || !__all(jl < 0 || wt < kWinSpan)) {
+                if (WP_COLD(!eok || !__all(jl < 0 || wt < kWinSpan))) {
 #pragma unroll
                     for (int u = 0; u < kWinBatch; ++u)
                         nv[u] = win_upd(x[ub + u], ib + u == r, jl == c, pw, mc[u], e);
                 }
 #pragma unroll
                 for (int u = 0; u < kWinBatch; ++u) x[ub + u] = jl >= 0 ? nv[u] : 0.0;
+                // lane u takes row u's multiplier, "-b" and entering-column entries (uniform
+                // lanes ms, cfs: read lanes, no LDS)
                 double myc = 0.0, mybv = 0.0, mya = 0.0;
 #pragma unroll
                 for (int u = 0; u < kWinBatch; ++u) {
-                    const double bvu = __shfl(nv[u], ms);
-                    const double au = cfs >= 0 ? __shfl(nv[u], cfs) : 0.0;
+                    const double bvu = readlane_d(nv[u], ms);
+                    const double au = cfs >= 0 ? readlane_d(nv[u], cfs) : 0.0;
                     if (lane == u) {
                         myc = mc[u];
                         mybv = bvu;
@@ -472,10 +551,11 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 }
                 const int i = ib + lane;
                 if (lane < kWinBatch && i < i1) {
-                    if (cfn != SMX_NONE && cfs < 0)
+                    if (WP_COLD(cfn != SMX_NONE && cfs < 0))
                         mya = win_upd(acv, i == r, cfn == c, s_prcf, myc, e);
                     mul[(int64_t)i * kBlkMax + D] = myc;
                     mT[(int64_t)D * (rows + 1) + i] = myc;
+                    s_mrow[wid][ub + lane][D] = myc;
                     if (want_x) {
                         if (i == hx0) xhist[hslot] = mybv;
                         if (i == hx1) xhist[hslot + 1] = mybv;
@@ -485,11 +565,27 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
             }
         }
         SMX_BLK_STAMP(5);
+        SMX_BLK_STAMP_WMAX(6);
         // ---- the records of step L: granules (L < P) or memory (the next block's first) -------
         {
             const int n0 = wave_min_int_dpp(R.nb);
             const First f0 = wave_first_dpp(R.f);
             const Cand c0 = wave_best_dpp(R.bc);
+            if (L < P) {
+                // this wave's candidate pivot row for step L, published now (see the header)
+                const int cr = n0 != SMX_NONE ? n0
+                             : (f0.idx != SMX_NONE && isnan(f0.v)) ? f0.idx
+                             : (c0.cls < 2 ? c0.idx : SMX_NONE);
+                uint64_t* __restrict__ cd =
+                    cand + ((int64_t)(L & 1) * NW + gw) * kWpCandG;
+                if (cr != SMX_NONE) {
+                    const int u = cr - i0;
+                    wp_put(cd + 2 + 2 * lane, tagL, xrow(u));
+                    if (lane < L) wp_put(cd + 2 + 2 * kWin + 2 * lane, tagL, s_mrow[wid][u][lane]);
+                }
+                if (lane == 0) st_sc1(cd, tagL | (uint32_t)(cr == SMX_NONE ? 0xFFFFFFFFu : (uint32_t)cr));
+                mycand = cr;
+            }
             if (lane == 0) s_r[wid] = BlkRec{n0, f0, c0};
             if (tid == 0) {
                 s_pv.c[D] = c;
@@ -497,27 +593,25 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 s_xm[1][D] = fc;
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (tid == 0) {
-                BlkRec a = s_r[0];
-                for (int w = 1; w < kWinWaves; ++w) {
-                    a.nb = min(a.nb, s_r[w].nb);
-                    if (s_r[w].f.idx < a.f.idx) a.f = s_r[w].f;
-                    if (better(s_r[w].bc, a.bc)) a.bc = s_r[w].bc;
-                }
-                smx_part pt;
-                pt.p1col = a.nb;
-                pt.first = a.f.idx;
-                pt.first_v = a.f.v;
-                pt.best_cls = a.bc.cls;
-                pt.best_i = a.bc.idx;
-                pt.best_v = a.bc.v;
+            SMX_BLK_STAMP(8);
+            if (wid == 0) {
+                // the eight waves' records: lane k < 8 takes wave k's, three DPP steps merge them
+                BlkRec a = s_r[lane & (kWinWaves - 1)];
+                a = wp_rec_merge(a, wp_rec_dpp<kDppXor1>(a));
+                a = wp_rec_merge(a, wp_rec_dpp<kDppXor2>(a));
+                a = wp_rec_merge(a, wp_rec_dpp<kDppHalfMirror>(a));
                 if (L < P) {
-                    uint32_t pl[kWpRecG];
-                    wp_pack(pt, pl);
-                    uint64_t* dst = rec + ((int64_t)(L & 1) * kWinMaxG + b) * kWpRecG;
-#pragma unroll
-                    for (int g = 0; g < kWpRecG; ++g) st_sc1(dst + g, tagL | pl[g]);
-                } else {
+                    if (lane < kWpRecG)
+                        st_sc1(rec + ((int64_t)(L & 1) * kWinMaxG + b) * kWpRecG + lane,
+                               tagL | wp_pack1(a, lane));
+                } else if (lane == 0) {
+                    smx_part pt;
+                    pt.p1col = a.nb;
+                    pt.first = a.f.idx;
+                    pt.first_v = a.f.v;
+                    pt.best_cls = a.bc.cls;
+                    pt.best_i = a.bc.idx;
+                    pt.best_v = a.bc.v;
                     parts[(int64_t)blk_slot(L, P, bn) * G + b] = pt;
                 }
             }

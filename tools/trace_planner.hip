@@ -79,10 +79,10 @@ int main(int argc, char** argv) {
                                      nullptr));
         CK(hipDeviceSynchronize());
         parity = (parity + P) & 1;
-        static unsigned long long tr[kBlkMax + 1][kBlkTraceParts][8];
+        static unsigned long long tr[kBlkMax + 1][kBlkTraceParts][kBlkTracePh];
         CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_blk_trace), sizeof(tr)));
         {
-            static const unsigned long long z[kBlkMax + 1][kBlkTraceParts][8] = {};
+            static const unsigned long long z[kBlkMax + 1][kBlkTraceParts][kBlkTracePh] = {};
             CK(hipMemcpyToSymbol(HIP_SYMBOL(g_blk_trace), z, sizeof(z)));
         }
         static unsigned fb[kBlkMax + 1][2];
@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
             printf("{\"rep\": %d, \"N\": %d, \"P\": %d, \"L\": %d, \"span_us\": %.2f, "
                    "\"gap_us\": %.2f, \"phase_us\": [",
                    rep, N, P, L, (tend - t0) * 0.01, gap);
-            for (int ph = 0; ph < 8; ++ph) {
+            for (int ph = 0; ph < kBlkTracePh; ++ph) {
                 std::vector<double> v;
                 for (int g = 0; g < G; ++g)
                     if (tr[L][g][ph]) v.push_back((tr[L][g][ph] - t0) * 0.01);
