@@ -397,18 +397,13 @@ struct BlkRec {
 };
 
 __device__ __forceinline__ void blk_rec_add(BlkRec& R, int i, double bv, bool has_a, double a) {
-    if (bv < 0.0 && i < R.nb) R.nb = i;                     // simplex.py:73-76
-    if (has_a && a != 0.0) {                                // simplex.py:112 (NaN counts)
-        const double v = bv / a;                            // simplex.py:115
-        if (i < R.f.idx) {
-            R.f.idx = i;
-            R.f.v = v;
-        }
-        if (!isnan(v)) {
-            const Cand x = classify(v, i);
-            if (better(x, R.bc)) R.bc = x;
-        }
-    }
+    // (branch-free, smx_common.hpp better(); the quotient is formed whether or not it counts)
+    R.nb = ((bv < 0.0) & (i < R.nb)) ? i : R.nb;            // simplex.py:73-76
+    const bool use = has_a & (a != 0.0);                    // simplex.py:112 (NaN counts)
+    const double v = bv / a;                                // simplex.py:115
+    R.f = first_sel(use & (i < R.f.idx), First{i, v}, R.f);
+    const Cand x = classify(v, i);
+    R.bc = cand_sel(use & !isnan(v) & better(x, R.bc), x, R.bc);
 }
 
 // The workgroup's record (thread 0 holds it afterwards; the others an unspecified value)

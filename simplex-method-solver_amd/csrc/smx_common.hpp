@@ -32,10 +32,16 @@ __device__ __forceinline__ Cand classify(double v, int idx) {
     return c;
 }
 
+// (Branch-free: the reductions below run these per lane, and "if (better(o, a)) a = o" on a
+// struct compiled to exec-masked branch regions -- ~770 instructions and ~1.8 us for a wave's
+// three reductions and a merge in the persistent planner, profiles/r06o/.  Same order.)
 __device__ __forceinline__ bool better(const Cand& a, const Cand& b) {
-    if (a.cls != b.cls) return a.cls < b.cls;
-    if (a.cls == 0) return (a.v > b.v) || (a.v == b.v && a.idx > b.idx);
-    return a.idx < b.idx;
+    const bool c0 = (a.v > b.v) | ((a.v == b.v) & (a.idx > b.idx));
+    const bool cx = a.idx < b.idx;
+    return (a.cls < b.cls) | ((a.cls == b.cls) & (a.cls == 0 ? c0 : cx));
+}
+__device__ __forceinline__ Cand cand_sel(bool t, const Cand& a, const Cand& b) {
+    return Cand{t ? a.cls : b.cls, t ? a.idx : b.idx, t ? a.v : b.v};
 }
 
 __device__ __forceinline__ Cand shfl_xor_cand(const Cand& a, int mask) {
@@ -51,6 +57,10 @@ struct First {
     int idx;
     double v;
 };
+
+__device__ __forceinline__ First first_sel(bool t, const First& a, const First& b) {
+    return First{t ? a.idx : b.idx, t ? a.v : b.v};
+}
 
 __device__ __forceinline__ First shfl_xor_first(const First& a, int mask) {
     First o;
@@ -69,7 +79,7 @@ __device__ __forceinline__ Cand wave_best(Cand a) {
 #pragma unroll
     for (int mask = 32; mask >= 1; mask >>= 1) {
         Cand o = shfl_xor_cand(a, mask);
-        if (better(o, a)) a = o;
+        a = cand_sel(better(o, a), o, a);
     }
     return a;
 }
@@ -78,7 +88,7 @@ __device__ __forceinline__ First wave_first(First a) {
 #pragma unroll
     for (int mask = 32; mask >= 1; mask >>= 1) {
         First o = shfl_xor_first(a, mask);
-        if (o.idx < a.idx) a = o;
+        a = first_sel(o.idx < a.idx, o, a);
     }
     return a;
 }
@@ -126,18 +136,18 @@ __device__ __forceinline__ Cand readlane_cand(const Cand& a, int l) {
 }
 __device__ __forceinline__ Cand wave_best_dpp(Cand a) {
     Cand o = dpp_cand<kDppXor1>(a);
-    if (better(o, a)) a = o;
+    a = cand_sel(better(o, a), o, a);
     o = dpp_cand<kDppXor2>(a);
-    if (better(o, a)) a = o;
+    a = cand_sel(better(o, a), o, a);
     o = dpp_cand<kDppHalfMirror>(a);
-    if (better(o, a)) a = o;
+    a = cand_sel(better(o, a), o, a);
     o = dpp_cand<kDppMirror>(a);
-    if (better(o, a)) a = o;
+    a = cand_sel(better(o, a), o, a);
     Cand r = readlane_cand(a, 0);
 #pragma unroll
     for (int l = 16; l < kWave; l += 16) {
         o = readlane_cand(a, l);
-        if (better(o, r)) r = o;
+        r = cand_sel(better(o, r), o, r);
     }
     return r;
 }
@@ -148,18 +158,18 @@ __device__ __forceinline__ First dpp_first(const First& a) {
 }
 __device__ __forceinline__ First wave_first_dpp(First a) {
     First o = dpp_first<kDppXor1>(a);
-    if (o.idx < a.idx) a = o;
+    a = first_sel(o.idx < a.idx, o, a);
     o = dpp_first<kDppXor2>(a);
-    if (o.idx < a.idx) a = o;
+    a = first_sel(o.idx < a.idx, o, a);
     o = dpp_first<kDppHalfMirror>(a);
-    if (o.idx < a.idx) a = o;
+    a = first_sel(o.idx < a.idx, o, a);
     o = dpp_first<kDppMirror>(a);
-    if (o.idx < a.idx) a = o;
+    a = first_sel(o.idx < a.idx, o, a);
     First r{__builtin_amdgcn_readlane(a.idx, 0), readlane_d(a.v, 0)};
 #pragma unroll
     for (int l = 16; l < kWave; l += 16) {
         o = First{__builtin_amdgcn_readlane(a.idx, l), readlane_d(a.v, l)};
-        if (o.idx < r.idx) r = o;
+        r = first_sel(o.idx < r.idx, o, r);
     }
     return r;
 }

@@ -212,9 +212,9 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wstep(
 #pragma unroll
             for (int u = 0; u < RU; ++u) {
                 n0 = min(n0, rp[u].p1col);
-                if (rp[u].first < fi.idx) fi = First{rp[u].first, rp[u].first_v};
+                fi = first_sel(rp[u].first < fi.idx, First{rp[u].first, rp[u].first_v}, fi);
                 const Cand o{rp[u].best_cls, rp[u].best_i, rp[u].best_v};
-                if (better(o, bq)) bq = o;
+                bq = cand_sel(better(o, bq), o, bq);
             }
             nb = wave_min_int_dpp(n0);
             f = wave_first_dpp(fi);
@@ -448,11 +448,10 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wstep(
         for (int u = 0; u < kWinBatch; ++u) {
             const double bvu = __shfl(nv[u], ms);
             const double au = cfs >= 0 ? __shfl(nv[u], cfs) : 0.0;
-            if (lane == u) {
-                myc = mc[u];
-                mybv = bvu;
-                mya = au;
-            }
+            const bool mine = lane == u;
+            myc = mine ? mc[u] : myc;
+            mybv = mine ? bvu : mybv;
+            mya = mine ? au : mya;
         }
         const int i = ib + lane;
         if (lane < kWinBatch && i < i1) {

@@ -88,8 +88,8 @@ __device__ __forceinline__ BlkRec wp_rec_dpp(const BlkRec& a) {
 }
 __device__ __forceinline__ BlkRec wp_rec_merge(BlkRec a, const BlkRec& o) {
     a.nb = min(a.nb, o.nb);
-    if (o.f.idx < a.f.idx) a.f = o.f;
-    if (better(o.bc, a.bc)) a.bc = o.bc;
+    a.f = first_sel(o.f.idx < a.f.idx, o.f, a.f);
+    a.bc = cand_sel(better(o.bc, a.bc), o.bc, a.bc);
     return a;
 }
 
@@ -265,9 +265,9 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
 #pragma unroll
             for (int u = 0; u < RU; ++u) {
                 n0 = min(n0, rp[u].p1col);
-                if (rp[u].first < fi.idx) fi = First{rp[u].first, rp[u].first_v};
+                fi = first_sel(rp[u].first < fi.idx, First{rp[u].first, rp[u].first_v}, fi);
                 const Cand o{rp[u].best_cls, rp[u].best_i, rp[u].best_v};
-                if (better(o, bq)) bq = o;
+                bq = cand_sel(better(o, bq), o, bq);
             }
             const int nb = wave_min_int_dpp(n0);
             const First f = wave_first_dpp(fi);
@@ -543,11 +543,10 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                 for (int u = 0; u < kWinBatch; ++u) {
                     const double bvu = readlane_d(nv[u], ms);
                     const double au = cfs >= 0 ? readlane_d(nv[u], cfs) : 0.0;
-                    if (lane == u) {
-                        myc = mc[u];
-                        mybv = bvu;
-                        mya = au;
-                    }
+                    const bool mine = lane == u;
+                    myc = mine ? mc[u] : myc;
+                    mybv = mine ? bvu : mybv;
+                    mya = mine ? au : mya;
                 }
                 const int i = ib + lane;
                 if (lane < kWinBatch && i < i1) {
