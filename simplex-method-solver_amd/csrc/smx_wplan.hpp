@@ -152,6 +152,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     __shared__ int s_tmp[kWinWaves];
     __shared__ BlkRec s_r[kWinWaves];
     __shared__ double s_pw[kWave];               // the pivot row's window
+    __shared__ double s_rv[kWinWaves][3][kWinBatch];   // row pass: "-b", entering, multiplier
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
     const int b = blockIdx.x, G = gridDim.x;
     const int C = m + 1;
@@ -517,16 +518,34 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
 #pragma unroll
                     for (int u = 0; u < kWinBatch; ++u) mc[u] = __shfl(mcv, u);
                 }
-                uint32_t wt = 0;
+                // lane u of the wave will take row u's multiplier (lane cs's old value), "-b"
+                // entry (lane ms's new value) and entering-column entry (lane cfs's): handed over
+                // through LDS by those three lanes, 8 writes each (read-lane + select chains cost
+                // ~100 instructions per batch)
+                if (__builtin_expect(cs >= 0, 1) && lane == cs) {
+#pragma unroll
+                    for (int u = 0; u < kWinBatch; ++u) s_rv[wid][2][u] = x[ub + u];
+                }
+                // the pivot row (one row of the grid) takes its own rule below, off the fast path
+                const bool pc = jl == c;
+                double num[kWinBatch];
 #pragma unroll
                 for (int u = 0; u < kWinBatch; ++u) {
                     const double a = x[ub + u] * e;
                     const double bq = pw * mc[u];
-                    const bool pc = jl == c;
-                    const double num = (ib + u == r) ? (pc ? 1.0 : -x[ub + u]) : (pc ? x[ub + u] : (a - bq));
-                    wt = max(wt, win_term(num));
-                    const double tq = num * ey;
-                    const double rr = fma(-e, tq, num);
+                    num[u] = pc ? x[ub + u] : (a - bq);
+                }
+                if (WP_COLD((unsigned)(r - ib) < (unsigned)kWinBatch)) {
+#pragma unroll
+                    for (int u = 0; u < kWinBatch; ++u)
+                        if (ib + u == r) num[u] = pc ? 1.0 : -x[ub + u];
+                }
+                uint32_t wt = 0;
+#pragma unroll
+                for (int u = 0; u < kWinBatch; ++u) {
+                    wt = max(wt, win_term(num[u]));
+                    const double tq = num[u] * ey;
+                    const double rr = fma(-e, tq, num[u]);
                     nv[u] = fma(rr, ey, tq);
                 }
                 if (WP_COLD(!eok || !__all(jl < 0 || wt < kWinSpan))) {
@@ -534,20 +553,22 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                     for (int u = 0; u < kWinBatch; ++u)
                         nv[u] = win_upd(x[ub + u], ib + u == r, jl == c, pw, mc[u], e);
                 }
+                // (lanes outside the window, jl < 0, hold zeros that stay zeros; nothing reads
+                // them unmasked)
 #pragma unroll
-                for (int u = 0; u < kWinBatch; ++u) x[ub + u] = jl >= 0 ? nv[u] : 0.0;
-                // lane u takes row u's multiplier, "-b" and entering-column entries (uniform
-                // lanes ms, cfs: read lanes, no LDS)
-                double myc = 0.0, mybv = 0.0, mya = 0.0;
+                for (int u = 0; u < kWinBatch; ++u) x[ub + u] = nv[u];
+                if (lane == ms) {
 #pragma unroll
-                for (int u = 0; u < kWinBatch; ++u) {
-                    const double bvu = readlane_d(nv[u], ms);
-                    const double au = cfs >= 0 ? readlane_d(nv[u], cfs) : 0.0;
-                    const bool mine = lane == u;
-                    myc = mine ? mc[u] : myc;
-                    mybv = mine ? bvu : mybv;
-                    mya = mine ? au : mya;
+                    for (int u = 0; u < kWinBatch; ++u) s_rv[wid][0][u] = nv[u];
                 }
+                if (cfs >= 0 && lane == cfs) {
+#pragma unroll
+                    for (int u = 0; u < kWinBatch; ++u) s_rv[wid][1][u] = nv[u];
+                }
+                const int l8 = lane & (kWinBatch - 1);
+                const double mybv = s_rv[wid][0][l8];
+                double mya = cfs >= 0 ? s_rv[wid][1][l8] : 0.0;
+                const double myc = __builtin_expect(cs >= 0, 1) ? s_rv[wid][2][l8] : mcv;
                 const int i = ib + lane;
                 if (lane < kWinBatch && i < i1) {
                     if (WP_COLD(cfn != SMX_NONE && cfs < 0))
@@ -567,9 +588,13 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         SMX_BLK_STAMP_WMAX(6);
         // ---- the records of step L: granules (L < P) or memory (the next block's first) -------
         {
-            const int n0 = wave_min_int_dpp(R.nb);
-            const First f0 = wave_first_dpp(R.f);
-            const Cand c0 = wave_best_dpp(R.bc);
+            // the wave's record: only lanes 0..7 hold rows (one per batch row), three DPP steps
+            R = wp_rec_merge(R, wp_rec_dpp<kDppXor1>(R));
+            R = wp_rec_merge(R, wp_rec_dpp<kDppXor2>(R));
+            R = wp_rec_merge(R, wp_rec_dpp<kDppHalfMirror>(R));
+            const int n0 = __builtin_amdgcn_readfirstlane(R.nb);
+            const First f0{__builtin_amdgcn_readfirstlane(R.f.idx), readlane_d(R.f.v, 0)};
+            const Cand c0 = readlane_cand(R.bc, 0);
             if (L < P) {
                 // this wave's candidate pivot row for step L, published now (see the header)
                 const int cr = n0 != SMX_NONE ? n0
