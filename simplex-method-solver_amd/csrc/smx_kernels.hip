@@ -608,8 +608,8 @@ int launch_blk_wplan(const double* T, const smx_shape& s, int P, int parity, int
                      int64_t log_cap, hipStream_t st) {
     hipLaunchKernelGGL(k_blk_wplan, dim3(win_groups(s.rows)), dim3(kWinNT), 0, st, T, s.ld,
                        s.rows, s.m, s.flen, fscan_of(s), P, parity, bn, done, g_block_nwin,
-                       win_rpw(s.rows), ctl, b.h[0], b.parts, b.mul[0], b.xg, log, xhist,
-                       log_cap);
+                       win_rpw(s.rows), ctl, b.h[0], b.parts, b.mul[0], b.pr[0], b.xg, log,
+                       xhist, log_cap);
     return (int)hipGetLastError();
 }
 
@@ -796,7 +796,9 @@ int launch_block_chain(double* buf0, double* buf1, const smx_shape& s, int parit
                                       xhist, log_cap, st, xrow, 0);
 #endif
         }
-        if (!err && use_window(s, sh)) err = launch_blk_prows(tin, s, Pb, bp, st);
+        // (the persistent planner builds the pivot rows itself where its column slices fit)
+        if (!err && use_window(s, sh) && !(wplan && wp_inpr(s.m + 1, win_groups(s.rows))))
+            err = launch_blk_prows(tin, s, Pb, bp, st);
         if (ev) (void)hipEventRecord(ev[2 * bn], st);
         const bool lastb = done + Pb >= k;   // its pivot-column pass publishes the chain
         if (!err)

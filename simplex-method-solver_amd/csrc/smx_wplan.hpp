@@ -35,6 +35,12 @@ constexpr int kWpRowG = 2 * kWin + 2 * kBlkMax;       // on-demand pivot row: wi
 constexpr int kWpCandG = 2 + 2 * kWin + 2 * kBlkMax;  // a wave's candidate: row, window, mults
 constexpr int kWpMaxRpw = 16;                         // rows per wave in registers (32,768 rows)
 constexpr int kWpMaxWaves = kWinMaxG * kWinWaves;
+// The pivot rows at every column (the sweep's operands, k_blk_prows' job) are built inside the
+// launch when every workgroup's column slice fits one wave: ceil(C / G) <= 64 columns
+__host__ __device__ __forceinline__ int wp_cols_per_group(int C, int G) { return (C + G - 1) / G; }
+__host__ __device__ __forceinline__ bool wp_inpr(int C, int G) {
+    return wp_cols_per_group(C, G) <= kWave;
+}
 
 // scratch (uint64 granules): records [2 parities][kWinMaxG][kWpRecG], on-demand pivot rows
 // [2][kWpRowG], candidates [2][G * kWinWaves][kWpCandG] (blk_xg_used(G) of them)
@@ -136,8 +142,8 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     const double* __restrict__ T, int64_t ld, int rows, int m, int flen, int fscan, int P,
     int parity, int bn, int done, int nwin, int rpw, smx_ctl* __restrict__ ctl,
     BlkHdr* __restrict__ h, smx_part* __restrict__ parts, double* __restrict__ mul,
-    uint64_t* __restrict__ xg, int32_t* __restrict__ log, double* __restrict__ xhist,
-    int64_t log_cap) {
+    double* __restrict__ pr, uint64_t* __restrict__ xg, int32_t* __restrict__ log,
+    double* __restrict__ xhist, int64_t log_cap) {
     __shared__ BlkPiv s_pv;                      // the block's pivots so far (r, c, e)
     __shared__ double s_mp[kBlkMax + 1][kBlkMax]; // [pivot t][step q]: mul[r_t][q]
     // the fallbacks' extra rows: [0] the current pivot row's multipliers, [1] the f-row's (fc_q)
@@ -153,6 +159,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     __shared__ BlkRec s_r[kWinWaves];
     __shared__ double s_pw[kWave];               // the pivot row's window
     __shared__ double s_rv[kWinWaves][3][kWinBatch];   // row pass: "-b", entering, multiplier
+    __shared__ double s_prv[kBlkMax][kWave];     // pivot rows at this workgroup's column slice
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
     const int b = blockIdx.x, G = gridDim.x;
     const int C = m + 1;
@@ -213,6 +220,24 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     };
     // the row of x[] this wave published as its candidate for the coming step (none yet)
     int mycand = SMX_NONE;
+    // The pivot rows at this workgroup's column slice [jb, jb + CPW) (wave 1, lane = column):
+    // pivot row q's values T_{k+q}[r_q][j] from T_k[r_q][j] through the pivots before it, with
+    // pivot row q's multipliers (s_mp[q]) and the earlier pivot rows' values there (s_prv) --
+    // k_blk_prows' chains, one row per step, run while wave 0 polls the next step's records.
+    const bool inpr = wp_inpr(C, G);
+    const int CPW = wp_cols_per_group(C, G);
+    const int jpr = b * CPW + lane;
+    const bool prlane = inpr && wid == 1 && lane < CPW && jpr < C;
+    double prx = 0.0;   // T_k[r_q][jpr] of the latest pivot row, loaded when it was decided
+    auto prow_at = [&](int q) {
+        double v = prx;
+#pragma unroll 1
+        for (int t = 0; t < q; ++t)
+            v = win_upd(v, s_pv.r[q] == s_pv.r[t], jpr == s_pv.c[t], s_prv[t][lane], s_mp[q][t],
+                        s_pv.e[t]);
+        s_prv[q][lane] = v;
+        pr[(int64_t)q * ld + jpr] = v;
+    };
     auto xrow = [&](int u) {   // x[u] for a uniform u
         double v = 0.0;
 #pragma unroll
@@ -228,6 +253,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         const uint64_t tagD = (uint64_t)(uint32_t)(done + D + 1) << 32;
         const uint64_t tagL = (uint64_t)(uint32_t)(done + L + 1) << 32;
         // ---- the records of step D: from memory at D = 0, else the granules of step D --------
+        if (prlane && D > 0) prow_at(D - 1);
         if (wid == 0) {
             if (D > 0) {
                 // every record at once (RU x 4 granule loads per lane in flight), again until all
@@ -319,6 +345,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
             return;
         }
         const int r = d.r;
+        if (prlane) prx = T[(int64_t)r * ld + jpr];
         // ---- the pivot row: the owner's candidate slot, or published on demand -----------------
         uint64_t* __restrict__ prow = prg + (int64_t)(L & 1) * kWpRowG;
         if (WP_COLD(r >= i0 && r < i1 && (D == 0 || mycand != r))) {
@@ -644,6 +671,32 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         fo = fn;
         cf = cfn;
         ++kpiv;
+    }
+    if (!inpr) return;   // (k_blk_prows builds the pivot rows and the flags)
+    // the block's last pivot row, then the sweep's per-row flags (k_blk_prows' second job): this
+    // wave's rows from their multipliers in LDS, the f-row (workgroup 0) from fc_q
+    if (prlane) prow_at(P - 1);
+    int32_t* __restrict__ fl = blk_rflags(mul, rows + 1);
+    if (lane < rpw && i0 + lane < i1) {
+        bool bnd = true, zero = false, piv = false;
+#pragma unroll 1
+        for (int q = 0; q < P; ++q) {
+            const double v = s_mrow[wid][lane][q];
+            bnd = bnd && bnd_or_zero(v);
+            zero = zero || (dbits(v) << 1) == 0;
+            piv = piv || i0 + lane == s_pv.r[q];
+        }
+        fl[i0 + lane] = blk_rflag(piv, bnd, zero);
+    }
+    if (b == 0 && tid == 0) {
+        bool bnd = true, zero = false;
+#pragma unroll 1
+        for (int q = 0; q < P; ++q) {
+            const double v = s_xm[1][q];
+            bnd = bnd && bnd_or_zero(v);
+            zero = zero || (dbits(v) << 1) == 0;
+        }
+        fl[rows] = blk_rflag(false, bnd, zero);
     }
 }
 
