@@ -105,13 +105,13 @@ struct BlkLayout {
     int64_t parts, mul, pr, fr, bytes, mul_slot, pr_slot, win, xg;
 };
 // the persistent window planner's granules (smx_wplan.hpp: records [2][256][4], on-demand pivot
-// rows [2][2 * 64 + 2 * kBlkMax], every wave's candidate row [2][256 * 8][2 + 2 * 64 + 2 * kBlkMax])
+// rows [2][2 * 64 + 2 * kBlkMax], every workgroup's candidate row [2][256][2 + 2 * 64 + 2 * kBlkMax])
 constexpr int64_t kBlkXgBytes =
-    (2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax) + 2 * 256 * 8 * (2 + 2 * kWin + 2 * kBlkMax)) * 8;
-// the granules a grid of G planner workgroups uses (the candidates stride by G * 8 waves): what
+    (2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax) + 2 * 256 * (2 + 2 * kWin + 2 * kBlkMax)) * 8;
+// the granules a grid of G planner workgroups uses (the candidates stride by G): what
 // k_blk_start zeroes
 __host__ __device__ __forceinline__ int64_t blk_xg_used(int G) {
-    return 2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax) + (int64_t)2 * G * 8 * (2 + 2 * kWin + 2 * kBlkMax);
+    return 2 * 256 * 4 + 2 * (2 * kWin + 2 * kBlkMax) + (int64_t)2 * G * (2 + 2 * kWin + 2 * kBlkMax);
 }
 inline int64_t blk_align(int64_t x) { return (x + 255) / 256 * 256; }
 inline BlkLayout blk_layout(int64_t R, int64_t ld, int nparts) {

@@ -12,14 +12,18 @@ namespace {
 // workgroup keeps its rows' window in REGISTERS for the whole block and the steps hand off
 // through tagged 8-byte granules ({32-bit payload, 32-bit tag}, relaxed agent-scope = sc1 stores
 // and loads, the resident loop's protocol, smx_resident.hpp).  Per step:
-//   * every workgroup publishes its record (4 granules) and every wave publishes its CANDIDATE
-//     pivot row -- the row its own record would nominate (phase 1: its first row with a negative
-//     "-b"; phase 2: its ratio-test winner, or its first candidate when that ratio is NaN) -- with
-//     that row's window and multipliers, as soon as its row pass is done;
+//   * every workgroup publishes its record (4 granules) and its CANDIDATE pivot row -- the row
+//     its record would nominate (phase 1: its first row with a negative "-b"; phase 2: its
+//     ratio-test winner, or its first candidate when that ratio is NaN) -- with that row's window
+//     and multipliers (each wave stages its own candidate's window in LDS; the merging wave
+//     publishes the workgroup's);
 //   * one wave per workgroup polls all records, decides (every workgroup identically), then
-//     fetches the winner's window from the owning wave's candidate slot -- one more round trip,
-//     the bytes already published.  Where the owner's candidate is another row (a NaN first
-//     candidate, the block's first step) the owner publishes the pivot row on demand instead;
+//     fetches the winner's window from the owning workgroup's candidate slot -- one more round
+//     trip, the bytes already published.  Where the owner's candidate is another row (a NaN first
+//     candidate in another wave, the block's first step) the owner publishes the pivot row on
+//     demand instead.  (One candidate per wave cost 2,048 x 1.4 KB of write-through granules per
+//     step -- ~70 MB per block that the following sweep paid for in HBM traffic: 469 vs 440 us
+//     per 24-pivot sweep at 8192^2, profiles/r06r/.)
 //   * every wave applies the pivot to its rows in registers.
 // No window traffic, no boundary; the pivots, multipliers, log and x-history go out as in the
 // launch form (plain stores, read after the kernel).  Co-residency: one workgroup per CU (G <=
@@ -32,9 +36,9 @@ namespace {
 // test) and the best candidate's ratio.
 constexpr int kWpRecG = 4;
 constexpr int kWpRowG = 2 * kWin + 2 * kBlkMax;       // on-demand pivot row: window, multipliers
-constexpr int kWpCandG = 2 + 2 * kWin + 2 * kBlkMax;  // a wave's candidate: row, window, mults
+constexpr int kWpCandG = 2 + 2 * kWin + 2 * kBlkMax;  // a candidate: row, window, multipliers
 constexpr int kWpMaxRpw = 16;                         // rows per wave in registers (32,768 rows)
-constexpr int kWpMaxWaves = kWinMaxG * kWinWaves;
+
 // The pivot rows at every column (the sweep's operands, k_blk_prows' job) are built inside the
 // launch when every workgroup's column slice fits one wave: ceil(C / G) <= 64 columns
 __host__ __device__ __forceinline__ int wp_cols_per_group(int C, int G) { return (C + G - 1) / G; }
@@ -43,11 +47,10 @@ __host__ __device__ __forceinline__ bool wp_inpr(int C, int G) {
 }
 
 // scratch (uint64 granules): records [2 parities][kWinMaxG][kWpRecG], on-demand pivot rows
-// [2][kWpRowG], candidates [2][G * kWinWaves][kWpCandG] (blk_xg_used(G) of them)
-static_assert((2 * kWinMaxG * kWpRecG + 2 * kWpRowG + 2 * kWpMaxWaves * kWpCandG) * 8 ==
+// [2][kWpRowG], candidates [2][G][kWpCandG] (blk_xg_used(G) of them)
+static_assert((2 * kWinMaxG * kWpRecG + 2 * kWpRowG + 2 * kWinMaxG * kWpCandG) * 8 ==
                   kBlkXgBytes,
               "granule scratch");
-static_assert(kWinWaves == 8, "blk_xg_used");
 
 __device__ __forceinline__ uint32_t wp_idx16(int i) { return i == SMX_NONE ? 0xFFFFu : (uint32_t)i; }
 __device__ __forceinline__ int wp_idx(uint32_t v) { return v == 0xFFFFu ? SMX_NONE : (int)v; }
@@ -82,6 +85,13 @@ __device__ __forceinline__ void wp_put(uint64_t* p, uint64_t tag, double v) {
 // Branches a step almost never takes (fallbacks for columns outside the window, the exact
 // division's redo, time-outs, terminal steps): laid out after the hot path
 #define WP_COLD(x) __builtin_expect(!!(x), 0)
+
+// The row a record would nominate as the pivot row if it won the decision
+__device__ __forceinline__ int wp_nominee(int nb, const First& f, const Cand& bc) {
+    return nb != SMX_NONE ? nb
+         : (f.idx != SMX_NONE && isnan(f.v)) ? f.idx
+         : (bc.cls < 2 ? bc.idx : SMX_NONE);
+}
 
 // Records of the 8 waves (lanes 0..7 of wave 0, one each): merged in every lane of the group
 template <int CTRL>
@@ -160,6 +170,9 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     __shared__ double s_pw[kWave];               // the pivot row's window
     __shared__ double s_rv[kWinWaves][3][kWinBatch];   // row pass: "-b", entering, multiplier
     __shared__ double s_prv[kBlkMax][kWave];     // pivot rows at this workgroup's column slice
+    __shared__ double s_cw[kWinWaves][kWave];    // each wave's candidate row's window
+    __shared__ int s_wc[kWinWaves];              // each wave's candidate row
+    __shared__ int s_gcand;                      // the workgroup's published candidate row
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid >> 6;
     const int b = blockIdx.x, G = gridDim.x;
     const int C = m + 1;
@@ -170,7 +183,6 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
     uint64_t* __restrict__ cand = prg + 2 * (int64_t)kWpRowG;           // [2][waves][kWpCandG]
     const int64_t spin = g_res_spin_ticks;
     const int gw = b * kWinWaves + wid;   // this wave's index in the grid
-    const int NW = G * kWinWaves;
     const int i0 = gw * rpw;
     const int i1 = min(rows, i0 + rpw);
     constexpr int RU = kBlkPartsMax / kWave;
@@ -218,8 +230,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         if (b == 0) h->peff = D;
         s_bail = 1;
     };
-    // the row of x[] this wave published as its candidate for the coming step (none yet)
-    int mycand = SMX_NONE;
+    if (tid == 0) s_gcand = SMX_NONE;   // the workgroup's published candidate (none yet)
     // The pivot rows at this workgroup's column slice [jb, jb + CPW) (wave 1, lane = column):
     // pivot row q's values T_{k+q}[r_q][j] from T_k[r_q][j] through the pivots before it, with
     // pivot row q's multipliers (s_mp[q]) and the earlier pivot rows' values there (s_prv) --
@@ -348,7 +359,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         if (prlane) prx = T[(int64_t)r * ld + jpr];
         // ---- the pivot row: the owner's candidate slot, or published on demand -----------------
         uint64_t* __restrict__ prow = prg + (int64_t)(L & 1) * kWpRowG;
-        if (WP_COLD(r >= i0 && r < i1 && (D == 0 || mycand != r))) {
+        if (WP_COLD(r >= i0 && r < i1 && (D == 0 || s_gcand != r))) {
             const int u = r - i0;
             wp_put(prow + 2 * lane, tagL, xrow(u));
             if (lane < D) wp_put(prow + 2 * kWin + 2 * lane, tagL, s_mrow[wid][u][lane]);
@@ -359,7 +370,8 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
             uint64_t lo = 0, hi = 0, mlo = 0, mhi = 0;
             bool demand = D == 0;
             if (!demand) {
-                const uint64_t* cs_ = cand + ((int64_t)(D & 1) * NW + r / rpw) * kWpCandG;
+                const uint64_t* cs_ =
+                    cand + ((int64_t)(D & 1) * G + r / (rpw * kWinWaves)) * kWpCandG;
                 for (;;) {
                     const uint64_t rg = ld_sc1(cs_);
                     lo = ld_sc1(cs_ + 2 + 2 * lane);
@@ -623,19 +635,10 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
             const First f0{__builtin_amdgcn_readfirstlane(R.f.idx), readlane_d(R.f.v, 0)};
             const Cand c0 = readlane_cand(R.bc, 0);
             if (L < P) {
-                // this wave's candidate pivot row for step L, published now (see the header)
-                const int cr = n0 != SMX_NONE ? n0
-                             : (f0.idx != SMX_NONE && isnan(f0.v)) ? f0.idx
-                             : (c0.cls < 2 ? c0.idx : SMX_NONE);
-                uint64_t* __restrict__ cd =
-                    cand + ((int64_t)(L & 1) * NW + gw) * kWpCandG;
-                if (cr != SMX_NONE) {
-                    const int u = cr - i0;
-                    wp_put(cd + 2 + 2 * lane, tagL, xrow(u));
-                    if (lane < L) wp_put(cd + 2 + 2 * kWin + 2 * lane, tagL, s_mrow[wid][u][lane]);
-                }
-                if (lane == 0) st_sc1(cd, tagL | (uint32_t)(cr == SMX_NONE ? 0xFFFFFFFFu : (uint32_t)cr));
-                mycand = cr;
+                // this wave's candidate pivot row for step L, staged in LDS (see the header)
+                const int cr = wp_nominee(n0, f0, c0);
+                if (cr != SMX_NONE) s_cw[wid][lane] = xrow(cr - i0);
+                if (lane == 0) s_wc[wid] = cr;
             }
             if (lane == 0) s_r[wid] = BlkRec{n0, f0, c0};
             if (tid == 0) {
@@ -655,6 +658,22 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                     if (lane < kWpRecG)
                         st_sc1(rec + ((int64_t)(L & 1) * kWinMaxG + b) * kWpRecG + lane,
                                tagL | wp_pack1(a, lane));
+                    // the workgroup's candidate: the staged window of the wave that holds it,
+                    // when that wave nominated the same row (else none: on demand)
+                    int gc = wp_nominee(a.nb, a.f, a.bc);
+                    const int wg = gc != SMX_NONE ? (gc - b * kWinWaves * rpw) / rpw : 0;
+                    if (gc != SMX_NONE && s_wc[wg] != gc) gc = SMX_NONE;
+                    uint64_t* __restrict__ cd = cand + ((int64_t)(L & 1) * G + b) * kWpCandG;
+                    if (gc != SMX_NONE) {
+                        wp_put(cd + 2 + 2 * lane, tagL, s_cw[wg][lane]);
+                        if (lane < L)
+                            wp_put(cd + 2 + 2 * kWin + 2 * lane, tagL,
+                                   s_mrow[wg][gc - (b * kWinWaves + wg) * rpw][lane]);
+                    }
+                    if (lane == 0) {
+                        st_sc1(cd, tagL | (uint32_t)(gc == SMX_NONE ? 0xFFFFFFFFu : (uint32_t)gc));
+                        s_gcand = gc;   // (read after the next step's decision barrier)
+                    }
                 } else if (lane == 0) {
                     smx_part pt;
                     pt.p1col = a.nb;
