@@ -6,12 +6,13 @@ the origin so the trajectory is a long phase-2 run), resident in HBM before timi
 A "step" is one pivot of the reference's get_solution loop (simplex.py:184-198): its selection
 (pick_element, :70-141) and its Jordan step over every element (recalculate_matrix, :143-177).
 At N = 1 on this table the steps run as block pivots: up to P pivots (the library's policy,
-smx_tune_block: 20 from 1 GiB -- this table's 2 GiB and config 5's 17 GB --, 12 from 256 MiB,
-10 from 48 MiB) are decided by one planner launch each (k_blk_wstep: the window planner keeps the
-first columns of every row current pivot by pivot, csrc/smx_window.hpp), the pivot rows at every
-column are derived once per block (k_blk_prows), and ONE sweep of the tableau (k_blk_sweep)
-applies all of them, so a sweep moves 16 B per element for P pivots (a chain of k pivots is cut
-into blocks of near-equal size: the driver's 20 pivots are ONE sweep of 20, the default 200 ten);
+smx_tune_block: 24 where the persistent window planner runs -- this table's 2 GiB --, else 20 from
+1 GiB, 12 from 256 MiB, 10 from 48 MiB) are decided by ONE persistent planner launch per block
+(k_blk_wplan: the first columns of every row kept current pivot by pivot in registers, the steps
+handing off through tagged granules, csrc/smx_wplan.hpp; it also derives the pivot rows at every
+column), and ONE sweep of the tableau (k_blk_sweep) applies all of them, so a sweep moves 16 B per
+element for P pivots (a chain of k pivots is cut into blocks of near-equal size: the driver's 20
+pivots are ONE sweep of 20, the sustained 200 nine of 22-23);
 bit-identical to one pivot per sweep.  After the timed region the
 line adds `sustained` (the next 200 pivots, HIP events around every sweep: the steady-state rate
 beside the burst) and times the one-pivot chain (k_update<kFused>, one kernel per pivot) as

@@ -346,8 +346,9 @@ int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear);
  * is in buf[(parity + d) & 1] (the sweep works in place when a block applies an even count).
  * Unsharded tableaux only (row0 = 0, rows = n).  `blk` is device scratch of smx_block_bytes
  * bytes (no initialisation needed).  smx_block_bytes: with *pivots_inout = 0 it asks the
- * library's policy (smx_tune_block: 0 automatic = 10 pivots for tables of 48..256 MiB, 12 from
- * 256 MiB, 20 from 1 GiB; 1 never, 2..24 that many) and returns 0 when chains of
+ * library's policy (smx_tune_block: 0 automatic = from 48 MiB on, 24 pivots where the persistent
+ * window planner runs, else 10 up to 256 MiB, 12 from 256 MiB, 20 from 1 GiB; 1 never, 2..24
+ * that many) and returns 0 when chains of
  * `shape` would not use blocks; with 1..24 it asks for that many (0: `shape` not eligible).  Otherwise it returns the scratch size and sets
  * *pivots_inout to the pivots per block.  smx_block_run_timed also returns each sweep's HIP-event time (ceil(k/pivots)
  * entries) and the chain's total. */

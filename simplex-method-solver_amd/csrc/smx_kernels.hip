@@ -474,7 +474,14 @@ constexpr int64_t kBlockWideTable = 256ll << 20;
 // sweeps at 803 / 773 / 743 / 744 us per pivot with 12 / 16 / 20 / 24 pivots per sweep, planner
 // 26 / 30 us per pivot at 12 / 20 (profiles/r05b/).  Below 1 GiB (8192^2: 32.0 / 33.6 / 36.1 us
 // at 12 / 14 / 16, where the planner's share is larger) it stays at 12.
+// Round 6, the persistent window planner (smx_wplan.hpp, ~8 us per pivot wherever it runs):
+// kBlkMax = 24 pivots per sweep is the fastest at every size measured (tools/block_bench.py,
+// profiles/r06s/, us per pivot at 8 / 12 / 16 / 20 / 24: 3072^2 13.3 / 12.5 / 12.0 / 11.8 / 11.7,
+// 4096^2 16.3 / 14.9 / 14.2 / 14.0 / 13.8, 6144^2 24.9 / 20.9 / 19.6 / 20.4 / 19.3; 8192^2 and
+// 16384^2 at 16 / 20 / 24 30.5 / 29.4 / 28.7 and 91.7 / 88.7 / 87.0, profiles/r06r/), so
+// tables it plans take 24; the others keep the launch-form policy above.
 constexpr int64_t kBlockHugeTable = 1ll << 30;
+bool wplan_shape(const smx_shape& s);
 
 int block_pivots(const smx_shape& s) {
     if (g_block == 1) return 0;
@@ -482,6 +489,7 @@ int block_pivots(const smx_shape& s) {
     if (g_block >= 2) return g_block;
     const int64_t bytes = (int64_t)(s.rows + 1) * s.ld * 8;
     if (bytes < kBlockMinTable) return 0;
+    if (wplan_shape(s)) return kBlkMax;
     if (bytes >= kBlockHugeTable) return 20;
     return bytes >= kBlockWideTable ? 12 : 10;
 }
@@ -558,6 +566,7 @@ bool use_wplan(const smx_shape& s, bool sh) {
     return use_window(s, sh) && g_block_planner == 0 && win_rpw(s.rows) <= kWpMaxRpw &&
            win_groups(s.rows) <= num_cus();
 }
+bool wplan_shape(const smx_shape& s) { return use_wplan(s, false); }
 
 // Planner workgroups of a chain (every launch of one chain uses the same count, since a step
 // merges the records of the step before it by that count)

@@ -339,8 +339,9 @@ def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
                                     ("degenerate_mixed", 41)])
 def test_block_wide_table_vs_oracle(block_mode, kind, k):
     """A 1 GiB table 4096 x 32768 (config 5's width: 256 chunks of 128 columns per row) through
-    the default policy, 20 pivots per sweep in the LDS layout, integer degenerate data included
-    (zeros: the zero-extended division; exact paths): 20 = one block, 41 = 14 + 14 + 13."""
+    the default policy, 24 pivots per sweep in the LDS layout (the persistent planner; its column
+    slices of 128 leave the pivot rows to k_blk_prows), integer degenerate data included (zeros:
+    the zero-extended division; exact paths): 20 = one block, 41 = 21 + 20."""
     from simplex_mi355x import lp
     from simplex_mi355x.device import DeviceTableau
     from oracle import c_oracle
@@ -348,7 +349,7 @@ def test_block_wide_table_vs_oracle(block_mode, kind, k):
     n, m = 4095, 32767
     T = lp.dense_tableau(kind, 5, n, m)
     dev = DeviceTableau(T, n, m, m)
-    assert dev.block_plan()[1] == 20
+    assert dev.block_plan()[1] == 24
     dev.run(k, graph=False)
     ctl = dev.sync_state()
     Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=16)
@@ -362,11 +363,19 @@ def test_block_wide_table_vs_oracle(block_mode, kind, k):
 def test_block_plan_policy(block_mode):
     from simplex_mi355x import _lib
     block_mode(0)
-    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 20   # 2 GiB
-    assert _lib.block_plan([32768, 32767, 32767, 32767, 32767, 0, 64])[1] == 20   # 8 GiB
+    # the persistent planner's tables (up to 32,768 rows): 24; beyond, the launch-form policy
+    assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 24   # 2 GiB
+    assert _lib.block_plan([32768, 32767, 32767, 32767, 32767, 0, 64])[1] == 24   # 8 GiB
     assert _lib.block_plan([32768, 65535, 65535, 32767, 32767, 0, 64])[1] == 20   # config 5
-    assert _lib.block_plan([8192, 8191, 8191, 8191, 8191, 0, 32])[1] == 12
-    assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 10
+    assert _lib.block_plan([8192, 8191, 8191, 8191, 8191, 0, 32])[1] == 24
+    assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 24
+    prev = _lib.tune_block_planner(2, 0)   # the launch form: round 5's policy
+    try:
+        assert _lib.block_plan([16384, 16383, 16383, 16383, 16383, 0, 64])[1] == 20
+        assert _lib.block_plan([8192, 8191, 8191, 8191, 8191, 0, 32])[1] == 12
+        assert _lib.block_plan([3072, 3071, 3071, 3071, 3071, 0, 12])[1] == 10
+    finally:
+        _lib.tune_block_planner(prev, 0)
     assert _lib.block_plan([2048, 2047, 2047, 2047, 2047, 0, 8]) is None    # below 48 MiB
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4]) is None
     assert _lib.block_plan([1024, 1023, 1023, 1023, 1023, 0, 4], 6)[1] == 6

@@ -27,6 +27,7 @@
 #   py=SCRIPT,ARGS         python3 SCRIPT ARGS (a tools/ probe)
 #   run=PROGRAM,ARGS       a built tools/ probe (e.g. `run=tools/cumask_probe`)
 #   pmcrun=C1:C2..,PROGRAM,ARGS  one rocprofv3 --pmc pass (counters ':'-separated) over a built probe
+#   pmcpy=C1:C2..,SCRIPT,ARGS    the same over a python script (python3 SCRIPT ARGS)
 # A recipe may carry its own time limit: `paths=...@300` (seconds; default per recipe below).
 set -o pipefail
 TAG=${1:?tag}
@@ -76,6 +77,7 @@ for spec in "$@"; do
     configs) cmd="cd $R && python -u tools/run_configs.py $arg"; d=600 ;;
     py) cmd="cd $R && python -u $arg"; d=300 ;;
     run) cmd="cd $R && $arg"; d=300 ;;
+    pmcpy) ctrs="${arg%% *}"; cmd="cd /tmp && timeout -s KILL 240 rocprofv3 --pmc ${ctrs//:/ } -d $O/$tag -o run --output-format csv -- python3 $R/${arg#* }"; d=280 ;;
     pmcrun) ctrs="${arg%% *}"; cmd="cd /tmp && timeout -s KILL 60 rocprofv3 --pmc ${ctrs//:/ } -d $O/$tag -o run --output-format csv -- $R/${arg#* }"; d=90 ;;
     *) echo "unknown recipe $name"; exit 2 ;;
   esac
