@@ -26,6 +26,7 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+#include <type_traits>
 #include <utility>
 #include <string.h>
 

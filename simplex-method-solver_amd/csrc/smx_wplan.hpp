@@ -539,90 +539,100 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
         const double ey = efd.y;
         const bool eok = efd.ok;
         BlkRec R{SMX_NONE, First{SMX_NONE, 0.0}, cand_none()};
+        // (one instantiation per batch size: tables of at most 8,192 rows hold 4 rows per wave,
+        // and an 8-row batch would compute 4 of them for nothing)
+        auto rowpass = [&](auto nbc) {
+            constexpr int NB = decltype(nbc)::value;
+            constexpr int UBMAX = NB < kWinBatch ? NB : kWpMaxRpw;
 #pragma unroll
-        for (int ub = 0; ub < kWpMaxRpw; ub += kWinBatch) {
-            if (ub == 0 || WP_COLD(ub < rpw)) {   // (a second batch from 16,385 rows on)
-                const int ib = i0 + ub;
-                double mcv = 0.0, acv = 0.0;
-                if (WP_COLD(cs < 0) && lane < kWinBatch && ib + lane < i1)
-                    mcv = win_chain(T, ld, ib + lane, c, D, s_pv, s_colc, mul);
-                if (WP_COLD(cfs < 0 && cfn != SMX_NONE) && lane < kWinBatch && ib + lane < i1)
-                    acv = win_chain(T, ld, ib + lane, cfn, D, s_pv, s_colf, mul);
-                // row u's multiplier T_{k+D}[ib + u][c]: lane cs of x (uniform), or the chain
-                double mc[kWinBatch], nv[kWinBatch];
-                if (__builtin_expect(cs >= 0, 1)) {
+            for (int ub = 0; ub < UBMAX; ub += NB) {
+                if (ub == 0 || WP_COLD(ub < rpw)) {   // (a second batch from 16,385 rows on)
+                    const int ib = i0 + ub;
+                    double mcv = 0.0, acv = 0.0;
+                    if (WP_COLD(cs < 0) && lane < NB && ib + lane < i1)
+                        mcv = win_chain(T, ld, ib + lane, c, D, s_pv, s_colc, mul);
+                    if (WP_COLD(cfs < 0 && cfn != SMX_NONE) && lane < NB && ib + lane < i1)
+                        acv = win_chain(T, ld, ib + lane, cfn, D, s_pv, s_colf, mul);
+                    // row u's multiplier T_{k+D}[ib + u][c]: lane cs of x (uniform), or the chain
+                    double mc[NB], nv[NB];
+                    if (__builtin_expect(cs >= 0, 1)) {
 #pragma unroll
-                    for (int u = 0; u < kWinBatch; ++u) mc[u] = readlane_d(x[ub + u], cs);
-                } else {
+                        for (int u = 0; u < NB; ++u) mc[u] = readlane_d(x[ub + u], cs);
+                    } else {
 #pragma unroll
-                    for (int u = 0; u < kWinBatch; ++u) mc[u] = __shfl(mcv, u);
-                }
-                // lane u of the wave will take row u's multiplier (lane cs's old value), "-b"
-                // entry (lane ms's new value) and entering-column entry (lane cfs's): handed over
-                // through LDS by those three lanes, 8 writes each (read-lane + select chains cost
-                // ~100 instructions per batch)
-                if (__builtin_expect(cs >= 0, 1) && lane == cs) {
-#pragma unroll
-                    for (int u = 0; u < kWinBatch; ++u) s_rv[wid][2][u] = x[ub + u];
-                }
-                // the pivot row (one row of the grid) takes its own rule below, off the fast path
-                const bool pc = jl == c;
-                double num[kWinBatch];
-#pragma unroll
-                for (int u = 0; u < kWinBatch; ++u) {
-                    const double a = x[ub + u] * e;
-                    const double bq = pw * mc[u];
-                    num[u] = pc ? x[ub + u] : (a - bq);
-                }
-                if (WP_COLD((unsigned)(r - ib) < (unsigned)kWinBatch)) {
-#pragma unroll
-                    for (int u = 0; u < kWinBatch; ++u)
-                        if (ib + u == r) num[u] = pc ? 1.0 : -x[ub + u];
-                }
-                uint32_t wt = 0;
-#pragma unroll
-                for (int u = 0; u < kWinBatch; ++u) {
-                    wt = max(wt, win_term(num[u]));
-                    const double tq = num[u] * ey;
-                    const double rr = fma(-e, tq, num[u]);
-                    nv[u] = fma(rr, ey, tq);
-                }
-                if (WP_COLD(!eok || !__all(jl < 0 || wt < kWinSpan))) {
-#pragma unroll
-                    for (int u = 0; u < kWinBatch; ++u)
-                        nv[u] = win_upd(x[ub + u], ib + u == r, jl == c, pw, mc[u], e);
-                }
-                // (lanes outside the window, jl < 0, hold zeros that stay zeros; nothing reads
-                // them unmasked)
-#pragma unroll
-                for (int u = 0; u < kWinBatch; ++u) x[ub + u] = nv[u];
-                if (lane == ms) {
-#pragma unroll
-                    for (int u = 0; u < kWinBatch; ++u) s_rv[wid][0][u] = nv[u];
-                }
-                if (cfs >= 0 && lane == cfs) {
-#pragma unroll
-                    for (int u = 0; u < kWinBatch; ++u) s_rv[wid][1][u] = nv[u];
-                }
-                const int l8 = lane & (kWinBatch - 1);
-                const double mybv = s_rv[wid][0][l8];
-                double mya = cfs >= 0 ? s_rv[wid][1][l8] : 0.0;
-                const double myc = __builtin_expect(cs >= 0, 1) ? s_rv[wid][2][l8] : mcv;
-                const int i = ib + lane;
-                if (lane < kWinBatch && i < i1) {
-                    if (WP_COLD(cfn != SMX_NONE && cfs < 0))
-                        mya = win_upd(acv, i == r, cfn == c, s_prcf, myc, e);
-                    mul[(int64_t)i * kBlkMax + D] = myc;
-                    mT[(int64_t)D * (rows + 1) + i] = myc;
-                    s_mrow[wid][ub + lane][D] = myc;
-                    if (want_x) {
-                        if (i == hx0) xhist[hslot] = mybv;
-                        if (i == hx1) xhist[hslot + 1] = mybv;
+                        for (int u = 0; u < NB; ++u) mc[u] = __shfl(mcv, u);
                     }
-                    blk_rec_add(R, i, mybv, cfn != SMX_NONE, mya);
+                    // lane u of the wave will take row u's multiplier (lane cs's old value), "-b"
+                    // entry (lane ms's new value) and entering-column entry (lane cfs's): handed over
+                    // through LDS by those three lanes, 8 writes each (read-lane + select chains cost
+                    // ~100 instructions per batch)
+                    if (__builtin_expect(cs >= 0, 1) && lane == cs) {
+#pragma unroll
+                        for (int u = 0; u < NB; ++u) s_rv[wid][2][u] = x[ub + u];
+                    }
+                    // the pivot row (one row of the grid) takes its own rule below, off the fast path
+                    const bool pc = jl == c;
+                    double num[NB];
+#pragma unroll
+                    for (int u = 0; u < NB; ++u) {
+                        const double a = x[ub + u] * e;
+                        const double bq = pw * mc[u];
+                        num[u] = pc ? x[ub + u] : (a - bq);
+                    }
+                    if (WP_COLD((unsigned)(r - ib) < (unsigned)NB)) {
+#pragma unroll
+                        for (int u = 0; u < NB; ++u)
+                            if (ib + u == r) num[u] = pc ? 1.0 : -x[ub + u];
+                    }
+                    uint32_t wt = 0;
+#pragma unroll
+                    for (int u = 0; u < NB; ++u) {
+                        wt = max(wt, win_term(num[u]));
+                        const double tq = num[u] * ey;
+                        const double rr = fma(-e, tq, num[u]);
+                        nv[u] = fma(rr, ey, tq);
+                    }
+                    if (WP_COLD(!eok || !__all(jl < 0 || wt < kWinSpan))) {
+#pragma unroll
+                        for (int u = 0; u < NB; ++u)
+                            nv[u] = win_upd(x[ub + u], ib + u == r, jl == c, pw, mc[u], e);
+                    }
+                    // (lanes outside the window, jl < 0, hold zeros that stay zeros; nothing reads
+                    // them unmasked)
+#pragma unroll
+                    for (int u = 0; u < NB; ++u) x[ub + u] = nv[u];
+                    if (lane == ms) {
+#pragma unroll
+                        for (int u = 0; u < NB; ++u) s_rv[wid][0][u] = nv[u];
+                    }
+                    if (cfs >= 0 && lane == cfs) {
+#pragma unroll
+                        for (int u = 0; u < NB; ++u) s_rv[wid][1][u] = nv[u];
+                    }
+                    const int l8 = lane & (NB - 1);
+                    const double mybv = s_rv[wid][0][l8];
+                    double mya = cfs >= 0 ? s_rv[wid][1][l8] : 0.0;
+                    const double myc = __builtin_expect(cs >= 0, 1) ? s_rv[wid][2][l8] : mcv;
+                    const int i = ib + lane;
+                    if (lane < NB && i < i1) {
+                        if (WP_COLD(cfn != SMX_NONE && cfs < 0))
+                            mya = win_upd(acv, i == r, cfn == c, s_prcf, myc, e);
+                        mul[(int64_t)i * kBlkMax + D] = myc;
+                        mT[(int64_t)D * (rows + 1) + i] = myc;
+                        s_mrow[wid][ub + lane][D] = myc;
+                        if (want_x) {
+                            if (i == hx0) xhist[hslot] = mybv;
+                            if (i == hx1) xhist[hslot + 1] = mybv;
+                        }
+                        blk_rec_add(R, i, mybv, cfn != SMX_NONE, mya);
+                    }
                 }
             }
-        }
+        };
+        if (rpw <= kWinBatch / 2)
+            rowpass(std::integral_constant<int, kWinBatch / 2>{});
+        else
+            rowpass(std::integral_constant<int, kWinBatch>{});
         SMX_BLK_STAMP(5);
         SMX_BLK_STAMP_WMAX(6);
         // ---- the records of step L: granules (L < P) or memory (the next block's first) -------

@@ -314,17 +314,18 @@ def test_block_terminal_state_matches_chain(block_mode):
 @pytest.mark.parametrize("n,m,k,P", [(8191, 8191, 23, 12), (16383, 16383, 9, 20),
                                      (16383, 16383, 20, 20), (16383, 16383, 47, 20),
                                      (3071, 3071, 13, 10)])
-def test_block_full_size_prefix_vs_oracle(block_mode, n, m, k, P):
-    """BASELINE sizes through the default policy (10, 12 or -- 1-4 GiB tables -- 20 pivots per
-    sweep at most, blocks of near-equal size: 23 = 12 + 11, 9 = one block, 20 = one block of 20
-    in the LDS layout (k_blk_sweep<20, 5>), 47 = 16 + 16 + 15, 13 = 7 + 6)."""
+def test_block_full_size_prefix_vs_oracle(block_mode, planner_form, n, m, k, P):
+    """BASELINE sizes through the default policy: with the launch-form planners 10, 12 or --
+    1-4 GiB tables -- 20 pivots per sweep at most, blocks of near-equal size (23 = 12 + 11, 9 = one
+    block, 20 = one block of 20 in the LDS layout (k_blk_sweep<20, 5>), 47 = 16 + 16 + 15, 13 =
+    7 + 6); with the persistent planner 24 (23, 9, 20 = one block, 47 = 24 + 23, 13 = one)."""
     from simplex_mi355x import lp, _lib
     from simplex_mi355x.device import DeviceTableau
     from oracle import c_oracle
     block_mode(0)
     T = lp.dense_tableau("uniform", 0, n, m)
     dev = DeviceTableau(T, n, m, m)
-    assert dev.block_plan()[1] == P
+    assert dev.block_plan()[1] == (24 if planner_form == 0 else P)
     dev.run(k, graph=False)
     ctl = dev.sync_state()
     Tref, st, done, log = c_oracle.run(T, n, m, m, k, threads=16)
