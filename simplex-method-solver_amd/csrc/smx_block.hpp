@@ -403,7 +403,7 @@ __device__ __forceinline__ void blk_rec_add(BlkRec& R, int i, double bv, bool ha
     const double v = bv / a;                                // simplex.py:115
     R.f = first_sel(use & (i < R.f.idx), First{i, v}, R.f);
     const Cand x = classify(v, i);
-    R.bc = cand_sel(use & !isnan(v) & better(x, R.bc), x, R.bc);
+    R.bc = cand_sel(((int)use & (int)!isnan(v) & (int)better(x, R.bc)) != 0, x, R.bc);
 }
 
 // The workgroup's record (thread 0 holds it afterwards; the others an unspecified value)

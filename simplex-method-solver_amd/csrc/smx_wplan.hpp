@@ -85,6 +85,10 @@ __device__ __forceinline__ void wp_put(uint64_t* p, uint64_t tag, double v) {
 // Branches a step almost never takes (fallbacks for columns outside the window, the exact
 // division's redo, time-outs, terminal steps): laid out after the hot path
 #define WP_COLD(x) __builtin_expect(!!(x), 0)
+// s_sleep operand between two polls of a hand-off (x 64 cycles; a build knob for power A/Bs)
+#ifndef WP_POLL_SLEEP
+#define WP_POLL_SLEEP 1
+#endif
 
 // The row a record would nominate as the pivot row if it won the decision
 __device__ __forceinline__ int wp_nominee(int nb, const First& f, const Cand& bc) {
@@ -288,7 +292,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                         bail(D);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(WP_POLL_SLEEP);
                 }
 #pragma unroll
                 for (int u = 0; u < RU; ++u) rp[u] = wp_unpack(w[u]);
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                         bail(D);   // (the workgroup leaves at the barrier below)
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(WP_POLL_SLEEP);
                 }
             }
             if (WP_COLD(demand)) {
@@ -409,7 +413,7 @@ __global__ __launch_bounds__(kWinNT) void k_blk_wplan(
                         bail(D);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(WP_POLL_SLEEP);
                 }
             }
             s_pw[lane] = wp_val(lo, hi);
