@@ -237,6 +237,26 @@ __device__ __forceinline__ double fd_zero(double n, double e, double y) {
     return __builtin_amdgcn_div_fixup(fma(r, y, t), e, n);
 }
 
+// The zero-extended domain without the fixup (round 6): divide by a = |e| > 0 with ya = |y| (the
+// refined reciprocal is sign-symmetric) and return the NEGATED quotient through the negated last
+// step, g = fma(-r, ya, -t) = -RN(r ya + t) (round-to-nearest is sign-symmetric: the same bits as
+// -fma(r, ya, t) for every nonzero quotient).  For a zero numerator and a > 0 it gives the right
+// signed zero, which the plain form gets wrong for one sign of the divisor: n = +0: t = +0,
+// r = RN(-0 + +0) = +0, g = RN(-0 + -0) = -0; n = -0: t = -0, r = RN(+0 + -0) = +0,
+// g = RN(-0 + +0) = +0.  So g = -(n / |e|) = -sgn(e) (n / e), bit for bit: the caller folds the
+// uniform sign -sgn(e) into the next step's product (blk_sweep_body_flag's s_zm) and applies the
+// last one once per element and block -- the same 6 fp64 instructions per element-pivot as the
+// unchecked fast path, where fd_zero takes 7.  All three negations are source modifiers.
+// SMX_ZNEG=0 (a build knob for A/B timing: make variant VFLAGS=-DSMX_ZNEG=0) keeps fd_zero there.
+#ifndef SMX_ZNEG
+#define SMX_ZNEG 1
+#endif
+__device__ __forceinline__ double fd_zneg(double n, double a, double ya) {
+    const double t = n * ya;
+    const double r = fma(-a, t, n);
+    return fma(-r, ya, -t);
+}
+
 // Self-check of the unchecked sequences on the domains the bounds guarantee (smx_fastdiv_check
 // bounded): out[0] = pairs with e in [2^-100, 2^101) and num = +0 or |num| in [2^-254, 2^410),
 // out[1] = those whose unchecked quotient differs from num / e in any bit; out[2] / out[3] the
@@ -262,9 +282,12 @@ __global__ __launch_bounds__(256) void k_fastdiv_bounded_check(const double* __r
             bad += (dbits(q) != dbits(ref)) ? 1 : 0;
         }
         if (z || (xe >= 1023u - 456u && xe < 1023u + 410u)) {
-            const double q = fd_zero(x, e, fd_prep(e).y);
+            const double y = fd_prep(e).y;
+            const double q = fd_zero(x, e, y);
+            // fd_zneg with the sign folded back: -sgn(e) * g
+            const double q2 = (e < 0.0 ? 1.0 : -1.0) * fd_zneg(x, fabs(e), fabs(y));
             ++in2;
-            bad2 += (dbits(q) != dbits(ref)) ? 1 : 0;
+            bad2 += (dbits(q) != dbits(ref) || dbits(q2) != dbits(ref)) ? 1 : 0;
         }
     }
     atomicAdd(&out[0], in);
@@ -1315,6 +1338,15 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
     constexpr bool LDS = FORM == 5;
     __shared__ dbl2 s_pr[LDS ? P : 1][kWave];
     __shared__ dbl2 s_ey[LDS ? P : 1];
+    // the zero-extended path's scalars (fd_zneg): the chain carries g_q = -sgn(e_q) x_{q+1}, so
+    // step q's product x_q e_q is g_{q-1} M_q with M_q = -sgn(e_{q-1}) e_q (M_0 = e_0, exact sign
+    // flips), the divisor |M_q| = |e_q| (a source modifier), the reciprocal |y_q|; the element
+    // after the block is s_zf g_{P-1}, s_zf = -sgn(e_{P-1})
+    // (the LDS layout only: in the register layout, whose e / y sit in scalar registers, the
+    // per-pivot LDS reads cost more than the fixup saved -- config 5 at 12 pivots per sweep, block
+    // 0 unchanged and the fast-path blocks 13 % slower, profiles/r06aa/)
+    __shared__ dbl2 s_zm[LDS ? P : 1];
+    __shared__ double s_zf;
     const int32_t* __restrict__ rfl = blk_rflags(mul, R);
     const int lane = threadIdx.x & (kWave - 1);
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1347,7 +1379,14 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
             s_pr[q][t % kWave] = jl < C ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + jl)
                                         : dbl2{0.0, 0.0};
         }
-        if (threadIdx.x < P) s_ey[threadIdx.x] = dbl2{h->e[threadIdx.x], h->y[threadIdx.x]};
+        if (threadIdx.x < P) {
+            const int q = threadIdx.x;
+            const double e = h->e[q];
+            s_ey[q] = dbl2{e, h->y[q]};
+            const double M = q == 0 ? e : (h->e[q - 1] < 0.0 ? e : -e);
+            s_zm[q] = dbl2{M, fabs(h->y[q])};
+            if (q == P - 1) s_zf = e < 0.0 ? 1.0 : -1.0;
+        }
         __syncthreads();
     } else {
 #pragma unroll
@@ -1473,7 +1512,10 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
             ok = true;
         } else if (chunk_zok && (rf & 1) && __all(bnd_or_zero(x0[0]) && bnd_or_zero(x0[1]))) {
             // the zero-extended domain (rf 1 or 3, a chunk or row with exact zeros): the same
-            // arithmetic with fd_zero's v_div_fixup (ONE more instruction per element-pivot)
+            // arithmetic, the division made zero-safe -- the register layout with fd_zero's
+            // v_div_fixup (one more instruction per element-pivot), the LDS layout with the
+            // sign-folded negated division (fd_zneg, s_zm: the fast path's instruction count;
+            // DESIGN 20.4)
             asm volatile("" ::: "memory");   // keeps this path out of the fast path's code
             SMX_PC(kPcZero);
             if constexpr (!LDS) {
@@ -1493,7 +1535,7 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                 }
             } else {
 #pragma unroll
-                for (int q = 0; q < P; ++q) {
+                for (int q = 0; q < P && !SMX_ZNEG; ++q) {
                     const dbl2 p = PR(q);
                     const dbl2 ey = EY(q);
                     const double e = ey[0], y = ey[1];
@@ -1502,7 +1544,18 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
                     n[1] = v0[1] * e - p[1] * pc0[q];
                     v0 = dbl2{fd_zero(n[0], e, y), fd_zero(n[1], e, y)};
                 }
+#pragma unroll
+                for (int q = 0; q < P && SMX_ZNEG; ++q) {
+                    const dbl2 p = PR(q);
+                    const dbl2 my = s_zm[q];
+                    const double M = my[0], ya = my[1];
+                    double n[2];
+                    n[0] = v0[0] * M - p[0] * pc0[q];
+                    n[1] = v0[1] * M - p[1] * pc0[q];
+                    v0 = dbl2{fd_zneg(n[0], fabs(M), ya), fd_zneg(n[1], fabs(M), ya)};
+                }
             }
+            if (LDS && SMX_ZNEG) v0 = dbl2{v0[0] * s_zf, v0[1] * s_zf};
             ok = true;
         } else if (allok && rf != 2) {   // not a pivot row (rf == 2): the window-tracked path
             // numerators checked once per row by a vote.  Exact zeros are inside the domain too
