@@ -258,8 +258,10 @@ def test_fastdiv_bounded_domain_matches_hardware_division():
     num = np.concatenate(nums)
     den = np.concatenate(dens)
     num[::97] = 0.0                    # +0 numerators (a zero numerator is never -0 there)
-    # the zero-extended domain of the flag-form sweep (fd_pos): -0 numerators over both signs of
-    # e, the -0.0 values of the edge fixtures, and numerators down to 2^-456
+    # the zero-extended domain of the flag-form sweep: -0 numerators over both signs of e, the
+    # -0.0 values of the edge fixtures, and numerators down to 2^-456 -- the kernel checks both
+    # zero-safe sequences there (fd_zero, and fd_zneg with its sign folded back), bad0 counting a
+    # pair either one gets wrong
     edge_zero = [v for rec in load("edge.json").values()
                  for row in dec_input(rec["input"])[0] for v in row if v == 0.0]
     assert any(math.copysign(1.0, v) < 0 for v in edge_zero)
