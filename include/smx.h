@@ -366,7 +366,9 @@ int smx_tune_block_planner(int32_t planner, int32_t nwin);
 /* Layout of the block sweep (k_blk_sweep, csrc/smx_block.hpp): 0 automatic (the default: pivot-
  * row slices in registers up to 12 pivots per sweep, in LDS shared by a workgroup's waves beyond,
  * and wherever the register layout's grid cannot give every wave one column chunk), 4 registers,
- * 5 LDS; any other value keeps the setting.  Returns the previous one.  Same bits either way. */
+ * 5 LDS, 6 LDS in work items (every workgroup's rows in K segments, each at another column chunk:
+ * SMX_SWEEP_ITEMS=K, default 16); any other value keeps the setting.  Returns the previous one.
+ * Same bits either way. */
 int smx_tune_block_form(int32_t form);
 int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout);
 int smx_block_run(double* buf0, double* buf1, const smx_shape* shape, int32_t parity, int32_t k,

@@ -1330,12 +1330,23 @@ __device__ unsigned long long g_path_cnt[kPcCount];
 #define SMX_PC_FLUSH ((void)0)
 #endif
 
+// FORM 6 (round 6): the LDS layout in work items.  A workgroup of FORM 5 keeps one chunk for all
+// its rows, so where a few chunks run a slower path (config 5's block 0: 5 of 257 chunks on the
+// window-tracked path) their workgroups finish last and the sweep waits for them (1.33x block 2's
+// cycles at 1.05x its instructions).  FORM 6 cuts every workgroup's rows into K
+// contiguous segments (K = g_sweep_items) and takes segment k at chunk (c0 + k * stride) mod
+// nchunks, stride ~ nchunks / K: for every k the map c0 -> chunk is a shift, so each (chunk,
+// segment) is still swept by exactly the workgroups that would have swept it, and a slow chunk's
+// rows spread over ~K times as many workgroups.  The pivot-row slices are restaged per item.
+__device__ int g_sweep_items = 16;
+
 template <int P, int FORM>
 __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* Tout, int64_t ld,
                                                     int R, int C, const BlkHdr* __restrict__ h,
                                                     const double* __restrict__ pr,
                                                     const double* __restrict__ mul) {
-    constexpr bool LDS = FORM == 5;
+    constexpr bool LDS = FORM >= 5;
+    constexpr bool ITEMS = FORM == 6;
     __shared__ dbl2 s_pr[LDS ? P : 1][kWave];
     __shared__ dbl2 s_ey[LDS ? P : 1];
     // the zero-extended path's scalars (fd_zneg): the chain carries g_q = -sgn(e_q) x_{q+1}, so
@@ -1360,10 +1371,17 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
     constexpr int kChunk = 2 * kWave;
     const int nchunks = (C + kChunk - 1) / kChunk;
     int ch, base, qs;
+    int c0 = 0, K = 1, stride = 1, seg = R;
     if constexpr (LDS) {
         ch = (int)blockIdx.x % nchunks;
         base = ((int)blockIdx.x / nchunks) * kUpdWaves + wib;
         qs = ((int)gridDim.x / nchunks) * kUpdWaves;
+        if constexpr (ITEMS) {
+            c0 = ch;
+            K = max(1, min(g_sweep_items, nchunks));
+            stride = max(1, nchunks / K);
+            seg = ((R + K - 1) / K + qs - 1) / qs * qs;   // a multiple of qs: the same interleave
+        }
     } else {
         const int NW = (int)gridDim.x * kUpdWaves;
         const int w = (int)blockIdx.x * kUpdWaves + wib;
@@ -1371,14 +1389,17 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         base = w / nchunks;
         qs = NW / nchunks;
     }
-    const int j = ch * kChunk + 2 * lane;
+    int j = ch * kChunk + 2 * lane;
     dbl2 prs[LDS ? 1 : P];
-    if constexpr (LDS) {
+    auto stage = [&]() {
         for (int t = threadIdx.x; t < P * kWave; t += kUpdBlock) {
             const int q = t / kWave, jl = ch * kChunk + 2 * (t % kWave);
             s_pr[q][t % kWave] = jl < C ? *reinterpret_cast<const dbl2*>(pr + (int64_t)q * ld + jl)
                                         : dbl2{0.0, 0.0};
         }
+    };
+    if constexpr (LDS) {
+        stage();
         if (threadIdx.x < P) {
             const int q = threadIdx.x;
             const double e = h->e[q];
@@ -1407,30 +1428,34 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
     };
     const bool kNoFree = g_blk_nofree != 0;
     SMX_PC_DECL
-    uint32_t et = 0, pt = 0;
-    bool zok = true;   // every pivot-row value bounded or an exact +-0
+    bool chunk_zok, chunk_free;
+    auto chunk_flags = [&]() {
+        uint32_t et = 0, pt = 0;
+        bool zok = true;   // every pivot-row value bounded or an exact +-0
 #pragma unroll
-    for (int q = 0; q < P; ++q) {
-        const dbl2 p = PR(q);
-        et = max(et, bnd_term(EY(q)[0]));
-        if (j < C) {
-            pt = max(pt, bnd_term(p[0]));
-            zok = zok && bnd_or_zero(p[0]);
+        for (int q = 0; q < P; ++q) {
+            const dbl2 p = PR(q);
+            et = max(et, bnd_term(EY(q)[0]));
+            if (j < C) {
+                pt = max(pt, bnd_term(p[0]));
+                zok = zok && bnd_or_zero(p[0]);
+            }
+            if (j + 1 < C) {
+                pt = max(pt, bnd_term(p[1]));
+                zok = zok && bnd_or_zero(p[1]);
+            }
         }
-        if (j + 1 < C) {
-            pt = max(pt, bnd_term(p[1]));
-            zok = zok && bnd_or_zero(p[1]);
-        }
-    }
-    // chunk_free: bounded, no zeros (fast path); chunk_zok: bounded or zero (zero-safe path)
-    const bool chunk_zok = !kNoFree && allok && et < kBndSpan && __all(zok);
-    const bool chunk_free = chunk_zok && __all(pt < kBndSpan);
+        // chunk_free: bounded, no zeros (fast path); chunk_zok: bounded or zero (zero-safe path)
+        chunk_zok = !kNoFree && allok && et < kBndSpan && __all(zok);
+        chunk_free = chunk_zok && __all(pt < kBndSpan);
+    };
+    chunk_flags();
     double eqa[P];   // the exact path's pivot elements (loaded there, rare)
     // Every vector load of the loop is this inline asm: a load the compiler can see (the slow
     // path's reload) made it put s_waitcnt vmcnt(0) at the head of the fast path, waiting for
     // the next row's prefetch before computing this row (sweep 990 us at P = 10, 16384^2, against
     // 750 us for the lab's loop, tools/sweep_lab.hip).
-    const int jc = min(j, (C - 1) & ~1);
+    int jc = min(j, (C - 1) & ~1);
     auto ldc = [&](int row) {
         dbl2 v;
         const double* p = Tin + (int64_t)min(row, R - 1) * ld + jc;
@@ -1602,22 +1627,44 @@ __device__ __forceinline__ void blk_sweep_body_flag(const double* Tin, double* T
         if (j < C)
             __builtin_nontemporal_store(v0, reinterpret_cast<dbl2*>(Tout + (int64_t)i0 * ld + j));
     };
-    if (base >= R) return;
-    // prefetch depth 1 over single rows: before a register set is used, the ops issued after
-    // its load are the previous row's store and the other set's load (vmcnt(2); vmcnt(1) first)
-    dbl2 a = ldc(base), b = ldc(base + qs);
-    asm volatile("s_waitcnt vmcnt(1)" : "+v"(a) :: "memory");
-    for (int i0 = base; i0 < R; i0 += 2 * qs) {
-        rowf(a, i0);
-        if (i0 + qs >= R) break;
-        a = ldc(i0 + 2 * qs);
-        asm volatile("s_waitcnt vmcnt(2)" : "+v"(b) :: "memory");
-        rowf(b, i0 + qs);
-        if (i0 + 2 * qs >= R) break;
-        b = ldc(i0 + 3 * qs);
-        asm volatile("s_waitcnt vmcnt(2)" : "+v"(a) :: "memory");
+    if constexpr (!ITEMS) {
+        if (base >= R) return;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int it = 0; it < K; ++it) {
+        int lo = 0, hi = R;
+        if constexpr (ITEMS) {
+            lo = it * seg;
+            hi = min(R, lo + seg);
+            if (it > 0) {
+                // the next item's chunk: every wave is done with the previous slices first
+                ch = (c0 + it * stride) % nchunks;
+                j = ch * kChunk + 2 * lane;
+                jc = min(j, (C - 1) & ~1);
+                __syncthreads();
+                stage();
+                __syncthreads();
+                chunk_flags();
+            }
+            if (lo + base >= hi) continue;   // (every wave still meets the barriers above)
+        }
+        // prefetch depth 1 over single rows: before a register set is used, the ops issued after
+        // its load are the previous row's store and the other set's load (vmcnt(2); vmcnt(1)
+        // first)
+        const int r0 = lo + base;
+        dbl2 a = ldc(r0), b = ldc(r0 + qs);
+        asm volatile("s_waitcnt vmcnt(1)" : "+v"(a) :: "memory");
+        for (int i0 = r0; i0 < hi; i0 += 2 * qs) {
+            rowf(a, i0);
+            if (i0 + qs >= hi) break;
+            a = ldc(i0 + 2 * qs);
+            asm volatile("s_waitcnt vmcnt(2)" : "+v"(b) :: "memory");
+            rowf(b, i0 + qs);
+            if (i0 + 2 * qs >= hi) break;
+            b = ldc(i0 + 3 * qs);
+            asm volatile("s_waitcnt vmcnt(2)" : "+v"(a) :: "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     SMX_PC_FLUSH;   // every exit of the loop lands here (diagnostic build only)
 }
 

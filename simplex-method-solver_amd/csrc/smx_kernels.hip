@@ -522,7 +522,8 @@ BlkSweepFn blk_sweep_pick(int P, std::integer_sequence<int, Is...>) {
 }
 BlkSweepFn blk_sweep_fn(int P, int form) {
     using All = std::make_integer_sequence<int, kBlkMax>;
-    return form == 5 ? blk_sweep_pick<5>(P, All{}) : blk_sweep_pick<4>(P, All{});
+    return form == 6 ? blk_sweep_pick<6>(P, All{})
+                     : form == 5 ? blk_sweep_pick<5>(P, All{}) : blk_sweep_pick<4>(P, All{});
 }
 
 template <bool SH, int... Is>
@@ -686,6 +687,7 @@ int launch_blk_publish(bool sh, const smx_shape& s, int parity, int bn, smx_ctl*
 // wave one chunk; 4 / 5 forced (tests, A/B timing).
 int g_block_form = 0;
 constexpr int kSweepRegMaxP = 12;
+constexpr int64_t kSweepItemRows = 2048;   // rows per wave from which FORM 6 is automatic
 
 // Grid of the LDS layout: a multiple of the chunks per row (every workgroup keeps one chunk),
 // as many workgroups as are resident at bpc per CU, at least one per chunk.
@@ -707,7 +709,7 @@ int launch_block_sweep(bool sh, double* tin, double* tother, const smx_shape& s,
                        int in_idx = 0, int ipx_part = 0, smx_ctl* pub_ctl = nullptr,
                        int pub_bn = 0, int pub_parity = 0) {
     const int nchunks = (s.m + 1 + 2 * kWave - 1) / (2 * kWave);
-    int form = g_block_form == 4 || g_block_form == 5 ? g_block_form
+    int form = g_block_form >= 4 && g_block_form <= 6 ? g_block_form
                                                       : (P > kSweepRegMaxP ? 5 : 4);
     int grid = 0;
     if (form == 4) {
@@ -718,7 +720,15 @@ int launch_block_sweep(bool sh, double* tin, double* tother, const smx_shape& s,
         if (((int64_t)grid * kUpdWaves) % nchunks != 0) form = 5;
     }
     BlkSweepFn fn = blk_sweep_fn(P, form);
-    if (form == 5)   // a grid of 8 workgroups per CU.  At P = 20 only 7 are resident (P KiB of
+    if (form == 5 && g_block_form == 0) {
+        // tall tables: the work-item layout (FORM 6), where each of a wave's K = 16 items keeps
+        // >= 128 rows -- config 5 (65536 rows: 2,341 rows per wave) 7 % faster per sweep, its
+        // block 0 12 % (a tail of slow chunks spread over the grid); at 16384^2 (256 rows per
+        // wave) it cost 7 %, at 8192^2 35 % (profiles/r06ag/)
+        const int64_t per = sweep_grid_lds(s, g_blocks_per_cu > 0 ? g_blocks_per_cu : 8) / nchunks;
+        if ((int64_t)(s.rows + 1) >= per * kUpdWaves * kSweepItemRows) form = 6;
+    }
+    if (form >= 5)   // a grid of 8 workgroups per CU.  At P = 20 only 7 are resident (P KiB of
                      // pivot-row slices in LDS, ~106 SGPRs), but the sweep is fp64-issue-bound
                      // there and the grid sized for 8 is as fast as 7 and faster than the
                      // occupancy API's 6: 16384^2, 200 pivots, mean sweep 1.464 / 1.488 / 1.503 ms
@@ -1568,7 +1578,7 @@ int smx_diag_path_counts(int64_t* out, int32_t count, int32_t clear) {
 
 int smx_tune_block_form(int32_t form) {
     const int prev = g_block_form;
-    if (form == 0 || form == 4 || form == 5) g_block_form = form;
+    if (form == 0 || (form >= 4 && form <= 6)) g_block_form = form;
     return prev;
 }
 
@@ -1592,6 +1602,10 @@ int64_t smx_block_bytes(const smx_shape* shape, int32_t* pivots_inout) {
         const char* e = getenv("SMX_BLK_NOFREE");
         const int v = (e && e[0] == '1') ? 1 : 0;
         if (v) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_blk_nofree), &v, sizeof v);
+        // SMX_SWEEP_ITEMS=K: work items per workgroup of the sweep's FORM 6 (default 16)
+        const char* it = getenv("SMX_SWEEP_ITEMS");
+        const int k = it ? atoi(it) : 0;
+        if (k > 0) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sweep_items), &k, sizeof k);
         return v;
     }();
     (void)nofree_env;

@@ -311,7 +311,8 @@ def tune_block_planner(planner: int = -1, nwin: int = -1) -> int:
 
 
 def tune_block_form(form: int = -1) -> int:
-    """smx_tune_block_form: 0 automatic, 4 pivot-row slices in registers, 5 in LDS; any other
+    """smx_tune_block_form: 0 automatic, 4 pivot-row slices in registers, 5 in LDS, 6 in LDS by
+    work items (rows in segments, each at another column chunk); any other
     value only queries; returns the previous setting."""
     return int(load().smx_tune_block_form(form))
 

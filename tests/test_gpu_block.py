@@ -49,7 +49,8 @@ def block_mode():
 
 @pytest.fixture
 def sweep_form():
-    """Set smx_tune_block_form (sweep layout 0 auto / 4 registers / 5 LDS) for one test."""
+    """Set smx_tune_block_form (sweep layout 0 auto / 4 registers / 5 LDS / 6 LDS work items)
+    for one test."""
     from simplex_mi355x import _lib
     prev = _lib.tune_block_form(-1)
     yield _lib.tune_block_form
@@ -68,8 +69,8 @@ def _solve(cons, func, cap, chunk):
                 table_hash(last.table))
 
 
-@pytest.mark.parametrize("P,form", [(2, 0), (3, 5), (4, 0), (8, 0), (8, 5), (11, 0), (16, 0),
-                                    (16, 4), (20, 0), (24, 5)])
+@pytest.mark.parametrize("P,form", [(2, 0), (3, 5), (3, 6), (4, 0), (8, 0), (8, 5), (11, 0),
+                                    (16, 0), (16, 4), (20, 0), (20, 6), (24, 5)])
 def test_every_fixture_block_vs_chain_vs_reference(block_mode, sweep_form, P, form):
     """Every trajectory fixture: block chain == one-pivot chain == the reference's pivots, with
     chunks that end inside and at block boundaries and terminal outcomes inside blocks."""
@@ -167,7 +168,7 @@ def test_window_fallbacks_vs_oracle(block_mode, planner_form, kind, n, m, k, chu
     ("degenerate_mixed", 900, 1300, 150, 75, 22),
     ("uniform", 255, 65535, 48, 48, 24),       # 512 chunks per row: one workgroup each
 ])
-@pytest.mark.parametrize("form", [0, 4, 5])
+@pytest.mark.parametrize("form", [0, 4, 5, 6])
 def test_block_vs_oracle(block_mode, sweep_form, kind, n, m, k, chunk, P, form):
     from oracle import c_oracle
     from simplex_mi355x import lp
@@ -189,7 +190,7 @@ def test_block_vs_oracle(block_mode, sweep_form, kind, n, m, k, chunk, P, form):
 
 
 @pytest.mark.parametrize("P", [10, 12, 16, 20, 24])
-@pytest.mark.parametrize("form", [4, 5])
+@pytest.mark.parametrize("form", [4, 5, 6])
 def test_block_bounded_fast_path_edges_vs_oracle(block_mode, sweep_form, P, form):
     """The one-row sweep's unchecked fast path (smx_block.hpp, kBndSpan) next to its fallbacks in
     one table: rows scaled past 2^101 (input bound), rows scaled to ~2^-60 (small numerators),
