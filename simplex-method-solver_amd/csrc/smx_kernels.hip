@@ -719,7 +719,6 @@ int launch_block_sweep(bool sh, double* tin, double* tother, const smx_shape& s,
         grid = update_grid(s, (const void*)blk_sweep_fn(P, 4), 0, 5);
         if (((int64_t)grid * kUpdWaves) % nchunks != 0) form = 5;
     }
-    BlkSweepFn fn = blk_sweep_fn(P, form);
     if (form == 5 && g_block_form == 0) {
         // tall tables: the work-item layout (FORM 6), where each of a wave's K = 16 items keeps
         // >= 128 rows -- config 5 (65536 rows: 2,341 rows per wave) 7 % faster per sweep, its
@@ -728,6 +727,7 @@ int launch_block_sweep(bool sh, double* tin, double* tother, const smx_shape& s,
         const int64_t per = sweep_grid_lds(s, g_blocks_per_cu > 0 ? g_blocks_per_cu : 8) / nchunks;
         if ((int64_t)(s.rows + 1) >= per * kUpdWaves * kSweepItemRows) form = 6;
     }
+    BlkSweepFn fn = blk_sweep_fn(P, form);
     if (form >= 5)   // a grid of 8 workgroups per CU.  At P = 20 only 7 are resident (P KiB of
                      // pivot-row slices in LDS, ~106 SGPRs), but the sweep is fp64-issue-bound
                      // there and the grid sized for 8 is as fast as 7 and faster than the
